@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py — the headline benchmark of BASELINE.json: Mpaths/s (+ Mrays/s) of the 1080p, 8-bounce,
+871,200-triangle dragon Cornell box (config C3), on N GPUs of one node.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config C3]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+A STEP is one progressive frame (1 spp, the reference's unit of work: one HalogenCompute dispatch + one
+accumulation blit, RP:324-347) over the whole 1920x1080 image PER GPU: at N GPUs one step traces N frames of
+the image, its 8x8 tiles dealt round-robin to the N ranks, so per-GPU work is fixed ("scaling": "weak") and the
+accumulated image is bit-identical to a 1-GPU render of N*K frames.  The timed region (barrier + device sync
+on both sides, max over ranks) covers K steps and, for N > 1, the final RCCL gather of the tiles to rank 0.
+Scene build/upload and BVH build are outside it (as in the reference meter, HalogenDebugUI.cs:37-56).
+
+value = W*H*N*K / time (Mpaths/s); Mrays/s counts get_ray_intersection calls (device counters).
+roofline: algorithmic bytes per trace launch (32 B per AABB test, 36 B per triangle test,
+64 B per mesh transform, 44 B per sphere test, 284 B per accepted hit, 48 B per pixel-frame) over the mean
+launch duration from HIP events on the launch stream, against 8 TB/s.
+cpu_baseline: the CPU oracle (oracle/hg_oracle.c, a scalar C restatement of the same kernel) on rank 0 at N=1,
+on a stratified sample of row bands of the same workload, threads = min(16, cpus).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "halogen-pathtracer_amd"))
+
+from halogen import abi  # noqa: E402
+from halogen import render_pass as rp  # noqa: E402
+from halogen import scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
+
+
+def algorithmic_bytes(c: dict) -> float:
+    return (32.0 * c["aabb_tests"] + 36.0 * c["tri_tests"] + 64.0 * c["mesh_visits"] + 44.0 * c["sphere_tests"]
+            + 284.0 * c["hits"] + 48.0 * c["paths"])
+
+
+def cpu_baseline(packed, params, cube, width, height, seconds, threads):
+    """Oracle on stratified 2-row bands of frame 1 until `seconds` of wall time are used."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import hg_oracle  # test-infra import, cpu_baseline leg only
+
+    hg_oracle.lib()
+    n_bands = 27
+    order = [int(b) for b in np.linspace(0, height - 2, n_bands).astype(int)]
+    paths = 0
+    t0 = time.perf_counter()
+    used = []
+    acc = np.zeros((height, width, 4), np.float32)
+    for y in order:
+        hg_oracle.render(packed, params, 1, True, acc=acc, cubemap=cube, pix_range=(y * width, (y + 2) * width),
+                         threads=threads)
+        paths += 2 * width
+        used.append(y)
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"{len(used)} stratified 2-row bands x {width} px of frame 1 ({paths} paths, {dt:.1f} s), "
+                      f"scalar C oracle (oracle/hg_oracle.c), {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--config", default="C3", choices=sorted(scenes.CONFIGS))
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--no-counters", action="store_true")
+    ap.add_argument("--save-image", default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    cfg = scenes.CONFIGS[args.config]
+    if args.width and args.height:
+        cfg = cfg.resized(args.width, args.height)
+    settings = scenes.settings_for(cfg)
+    s = rp.clamp_settings(settings)
+    t_setup = time.perf_counter()
+    packed = cfg.build_scene().pack()
+    cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
+    W, H = cfg.width, cfg.height
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
+
+    ctx = abi.Context(local_rank)
+    if args.block:
+        ctx.set_option(abi.HG_OPT_BLOCK, args.block)
+    if args.no_counters:
+        ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.upload_scene(packed)
+    if cube is not None:
+        ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+    ctx.resize(W, H)
+    ctx.set_tiling(rank, world)
+    ctx.set_params(params)
+    setup_s = time.perf_counter() - t_setup
+
+    frames_per_step = world  # per-GPU work fixed: one frame-equivalent of the image per GPU per step
+    for _ in range(args.warmup):
+        ctx.render(frames_per_step, True)
+    ctx.synchronize()
+    # timed region renders frames 1 .. K*N from a cleared accumulator (the C3 image at K=64, N=1)
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.reset_counters()
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.render(frames_per_step, True)
+    gathered = None
+    if dist is not None:
+        import torch
+
+        from halogen import distributed as hd
+
+        n_local = ctx.local_tile_count()
+        local = torch.empty((n_local, 64, 4), dtype=torch.float32, device=f"cuda:{local_rank}")
+        ctx.copy_tiles_device(local.data_ptr(), local.numel() * 4)
+        gathered = hd.gather_tiles(local, rank, world, W, H)
+    barrier()
+    dt = time.perf_counter() - t0
+
+    cnt = ctx.counters()
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        keys = ["paths", "rays", "tri_tests", "aabb_tests", "mesh_visits", "sphere_tests", "hits"]
+        v = torch.tensor([float(cnt[k]) for k in keys], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(v)
+        totals = dict(zip(keys, (int(x) for x in v.tolist())))
+    else:
+        totals = cnt
+
+    total_paths = W * H * frames_per_step * args.steps
+    result = None
+    if rank == 0:
+        launches = max(cnt["launches"], 1)
+        mean_launch_s = cnt["kernel_ms"] / 1e3 / launches
+        counters_ok = not args.no_counters and cnt["paths"] > 0
+        bytes_per_launch = algorithmic_bytes(cnt) / launches if counters_ok else None
+        achieved = bytes_per_launch / mean_launch_s / 1e9 if counters_ok and mean_launch_s > 0 else None
+        traffic = None
+        tfile = ROOT / "profiles" / "pmc_traffic.json"
+        if tfile.exists():
+            try:
+                t = json.loads(tfile.read_text())
+                if t.get("config") == args.config and t.get("width") == W and t.get("height") == H:
+                    traffic = t.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": METRIC,
+            "value": total_paths / dt / 1e6,
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (scene rebuilt from the reference's scene constants; Dragon_8k.fbx subdivided 10x)",
+            "config": {"workload": cfg.name, "width": W, "height": H, "frames_per_step": frames_per_step,
+                       "spp_total": frames_per_step * args.steps, "max_bounces": s["MaxBounces"],
+                       "triangles": len(packed.triangles), "blas_nodes": len(packed.blas),
+                       "parallelism": f"tiles{world}"},
+            "mrays_per_s": totals["rays"] / dt / 1e6 if counters_ok else None,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_launch_ms": mean_launch_s * 1e3,
+                         "kernel": "hg_trace_kernel"},
+            "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
+                                  ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
+            "setup_s": setup_s,
+            "cpu_baseline": None,
+        }
+        if args.save_image:
+            img = gathered.cpu().numpy() if gathered is not None else ctx.readback(W, H)
+            np.save(args.save_image, img)
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            result["cpu_baseline"] = cpu_baseline(packed, params, cube, W, H, args.cpu_seconds, threads)
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,76 @@
+// hg_layout.h — device-side data layout of the Halogen scene in HBM (private to libhalogen_hip.so).
+//
+// The ABI structs (include/halogen_abi.h) are the reference's AoS C# layouts.  hg_upload_scene repacks
+// them once into the layout below, chosen for the gfx950 traversal loop:
+//
+//   node records   64 B per BLAS entry, CHILD-PAIR form: record g holds the boxes of g's two children and
+//                  their node refs, so popping an inner node costs exactly one 64-B record fetch (4 x
+//                  dwordx4) and the reference's re-read of the popped node (HalgoenCompute.compute:405)
+//                  disappears.  Records of leaf entries are never read.
+//   leaf table     8 B per BLAS entry: (global first triangle, triangle count) — read only for leaves.
+//   node ref       uint32: bit 31 = leaf, bits 0..30 = global BLAS index (= accelerationBufferOffset +
+//                  mesh-relative index).  Decided at upload from triangleCount, so the kernel never has to
+//                  read a node to know what it is.
+//   triangles      36 B per triangle in three streams: tri_a = (v0.xyz, e1.x), tri_b = (e1.yz, e2.xy),
+//                  tri_c = e2.z, where e1 = v1 - v0 and e2 = v2 - v0 are the reference's own first two
+//                  subtractions (:312-313) done once on the host with the same IEEE operation.
+//   normals        48 B per triangle (n0, n1 - n0, n2 - n0), read once per accepted hit.
+//   meshes         80 B per mesh: full worldToLocal (16 floats, Unity column-major), root ref, triangle
+//                  offset, material index.
+//   spheres        48 B: (centre, radius), (cornerA, material bits), (cornerB, 0).
+//   materials      80 B: albedo; (specular.rgb, metallic); (emissive.rgb*intensity, roughness);
+//                  (absorption.xyz, ior); (priority, medium id, roughness^2, 0).
+//   accumulation   float4 per pixel, TILE-MAJOR: 8x8 tiles of 1 KiB, local tile t holds global tile
+//                  rank + t*n_ranks, pixel (lx,ly) at lx + 8*ly — one wave writes one contiguous KiB.
+#pragma once
+#include <stdint.h>
+
+#define HG_LEAF_BIT 0x80000000u
+#define HG_TILE 8
+#define HG_MAX_CUBE_MIPS 16
+
+struct HgDevMesh {
+    float w2l[16];
+    uint32_t root_ref;
+    uint32_t tri_offset;
+    uint32_t material;
+    uint32_t pad;
+};
+
+// Everything the trace kernel needs, passed by value as the kernel argument.
+struct HgKernelParams {
+    // camera (rows 0..2 of CamLocalToWorldMatrix, row-major: cam[r*4+c] = M(r,c))
+    float cam[12];
+    float W, H;
+    uint32_t Wu, Hu;
+    float vw, vh, near_, far_;
+    float focal_disc_radius;  // tan(radians(focalConeAngle)) * near, evaluated on the host with hg_fmath.h
+    float psx, psy;           // (vw*2)/W, (vh*2)/H
+    float filter_radius, focal_dist;
+    uint32_t spp, max_bounces, max_diff, max_glossy, max_trans;
+    uint32_t debug_mode, tri_range, box_range;
+    int32_t default_mip;
+    int32_t use_cube;
+    int32_t n_spheres, n_meshes;
+    int32_t first_frame, n_frames, accumulate;
+    // tiling
+    int32_t tiles_x, rank, n_ranks, n_local_tiles;
+    uint32_t stack_depth;  // LDS traversal stack entries per lane
+    // cubemap
+    int32_t cube_size, cube_mips;
+    uint32_t cube_mip_offset[HG_MAX_CUBE_MIPS];  // in float4 texels
+    // scene
+    const float4* __restrict__ spheres;
+    const HgDevMesh* __restrict__ meshes;
+    const float4* __restrict__ materials;
+    const float4* __restrict__ nodes;
+    const uint2* __restrict__ leaves;
+    const float4* __restrict__ tri_a;
+    const float4* __restrict__ tri_b;
+    const float* __restrict__ tri_c;
+    const float4* __restrict__ normals;
+    const float4* __restrict__ cube;
+    // outputs
+    float4* __restrict__ acc;
+    unsigned long long* __restrict__ counters;  // 7 x u64, order of hg_counters' first 7 fields
+};

@@ -1,0 +1,554 @@
+// hg_runtime.hip — implementation of the C-ABI in include/halogen_abi.h (context, uploads, dispatch,
+// readback, counters).  Stands in for the ComputeBuffer / RTHandle / DispatchCompute / Blit calls of
+// Assets/Scripts/Render Features/HalogenRenderPass.cs (RP:237-508).
+//
+// Error model: every entry point returns HG_OK or a negative HG_E_* code and never aborts; the text of
+// the last error is kept per context (hg_last_error).  There is no CPU fallback: a missing GPU or a HIP
+// failure is an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "halogen_abi.h"
+#include "hg_fmath.h"
+#include "hg_layout.h"
+
+hipError_t hg_launch_trace(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+
+namespace {
+
+constexpr uint32_t kMaxStack = 64;  // LDS stack entries per lane; BLAS depth must be <= kMaxStack - 2
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct hg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // scene
+    bool has_scene = false;
+    DevBuf spheres, meshes, materials, nodes, leaves, tri_a, tri_b, tri_c, normals;
+    int32_t n_spheres = 0, n_meshes = 0, n_materials = 0, n_tris = 0, n_nodes = 0;
+    uint32_t stack_depth = 2;
+
+    // cubemap
+    DevBuf cube;
+    int32_t cube_size = 0, cube_mips = 0;
+    uint32_t cube_mip_offset[HG_MAX_CUBE_MIPS] = {};
+
+    // params
+    bool has_params = false;
+    hg_params params{};
+
+    // target
+    int32_t W = 0, H = 0, rank = 0, n_ranks = 1, tiles_x = 0, tiles_y = 0, n_local_tiles = 0;
+    DevBuf acc;
+
+    // counters / timing
+    DevBuf counters_dev;
+    hg_counters counters{};
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events;
+
+    // options
+    int32_t kernel = HG_KERNEL_MEGA, block = 256, counters_on = 1;
+};
+
+namespace {
+
+int fail(hg_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HG_HIP(ctx, call)                                                                              \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess) return fail((ctx), HG_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+int set_device(hg_ctx* c) {
+    HG_HIP(c, hipSetDevice(c->device));
+    return HG_OK;
+}
+
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int upload(hg_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    size_t alloc = std::max<size_t>(bytes, 16);  // the reference allocates >= 1 element (RP:544)
+    if (b.bytes != alloc) {
+        release(b);
+        hipError_t e = hipMalloc(&b.p, alloc);
+        if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipMalloc(%zu) failed: %s", alloc, hipGetErrorString(e));
+        b.bytes = alloc;
+    }
+    if (bytes) HG_HIP(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return HG_OK;
+}
+
+float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+float bits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+int drain_events(hg_ctx* c) {
+    if (c->pending.empty()) return HG_OK;
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    for (auto& pr : c->pending) {
+        float ms = 0.0f;
+        HG_HIP(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+        c->counters.kernel_ms += double(ms);
+        c->free_events.push_back(pr);
+    }
+    c->pending.clear();
+    return HG_OK;
+}
+
+int alloc_target(hg_ctx* c) {
+    c->tiles_x = (c->W + HG_TILE - 1) / HG_TILE;
+    c->tiles_y = (c->H + HG_TILE - 1) / HG_TILE;
+    const int64_t total = int64_t(c->tiles_x) * c->tiles_y;
+    c->n_local_tiles = total > c->rank ? int32_t((total - c->rank + c->n_ranks - 1) / c->n_ranks) : 0;
+    const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
+    release(c->acc);
+    if (bytes) {
+        hipError_t e = hipMalloc(&c->acc.p, bytes);
+        if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipMalloc(accumulation %zu) failed", bytes);
+        c->acc.bytes = bytes;
+        HG_HIP(c, hipMemsetAsync(c->acc.p, 0, bytes, c->stream));
+    }
+    return HG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hg_abi_version(void) { return HG_ABI_VERSION; }
+
+int hg_create(int device, hg_ctx** out) {
+    if (!out) return HG_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return HG_E_HIP;
+    if (device < 0 || device >= n) return HG_E_INVALID;
+    hg_ctx* c = new hg_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->counters_dev.p, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return HG_E_HIP;
+    }
+    c->counters_dev.bytes = 16 * sizeof(unsigned long long);
+    if (hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes) != hipSuccess) {
+        delete c;
+        return HG_E_HIP;
+    }
+    *out = c;
+    return HG_OK;
+}
+
+void hg_destroy(hg_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
+                      &c->normals, &c->cube, &c->acc, &c->counters_dev})
+        release(*b);
+    for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : c->free_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* hg_last_error(const hg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, const HalogenMeshData* meshes,
+                    int32_t n_meshes, const PackedHalogenMaterial* materials, int32_t n_materials,
+                    const HalogenTriangle* tris, int32_t n_tris, const BVHEntry* blas, int32_t n_nodes) {
+    if (!c) return HG_E_INVALID;
+    if (n_spheres < 0 || n_meshes < 0 || n_materials < 0 || n_tris < 0 || n_nodes < 0)
+        return fail(c, HG_E_INVALID, "negative count");
+    if ((n_spheres && !spheres) || (n_meshes && !meshes) || (n_materials && !materials) || (n_tris && !tris) ||
+        (n_nodes && !blas))
+        return fail(c, HG_E_INVALID, "null array with non-zero count");
+    if (n_materials > 255)
+        return fail(c, HG_E_UNSUPPORTED, "at most 255 materials (medium stack packs material indices in bytes)");
+    if (int rc = set_device(c)) return rc;
+    c->has_scene = false;
+
+    // ---- spheres
+    std::vector<float4> sph(size_t(n_spheres) * 3);
+    for (int i = 0; i < n_spheres; ++i) {
+        const HalogenSphere& s = spheres[i];
+        if (s.materialIndex >= uint32_t(n_materials))
+            return fail(c, HG_E_INVALID, "sphere %d: materialIndex %u out of range", i, s.materialIndex);
+        sph[3 * i] = f4(s.center.x, s.center.y, s.center.z, s.radius);
+        sph[3 * i + 1] = f4(s.boundingCornerA.x, s.boundingCornerA.y, s.boundingCornerA.z, bits(s.materialIndex));
+        sph[3 * i + 2] = f4(s.boundingCornerB.x, s.boundingCornerB.y, s.boundingCornerB.z, 0.0f);
+    }
+    // ---- materials
+    std::vector<float4> mat(size_t(n_materials) * 5);
+    for (int i = 0; i < n_materials; ++i) {
+        const PackedHalogenMaterial& m = materials[i];
+        mat[5 * i] = f4(m.albedo.x, m.albedo.y, m.albedo.z, m.albedo.w);
+        mat[5 * i + 1] = f4(m.specularAlbedo.x, m.specularAlbedo.y, m.specularAlbedo.z, m.metallic);
+        // emissive.rgb * emissive.a (:901) and roughness^2 (:699) are the kernel's own operations done once here
+        mat[5 * i + 2] = f4(m.emissive.x * m.emissive.w, m.emissive.y * m.emissive.w, m.emissive.z * m.emissive.w,
+                            m.roughness);
+        mat[5 * i + 3] = f4(m.rayMedium.absorption.x, m.rayMedium.absorption.y, m.rayMedium.absorption.z,
+                            m.rayMedium.indexOfRefraction);
+        mat[5 * i + 4] = f4(bits(m.rayMedium.priority), bits(m.rayMedium.materialID), m.roughness * m.roughness, 0.0f);
+    }
+    // ---- triangles
+    const size_t nt = size_t(n_tris);
+    std::vector<float4> ta(nt), tb(nt), nrm(nt * 3);
+    std::vector<float> tc(nt);
+    for (int64_t t = 0; t < n_tris; ++t) {
+        const HalogenTriangle& h = tris[t];
+        const float e1x = h.pointB.x - h.pointA.x, e1y = h.pointB.y - h.pointA.y, e1z = h.pointB.z - h.pointA.z;
+        const float e2x = h.pointC.x - h.pointA.x, e2y = h.pointC.y - h.pointA.y, e2z = h.pointC.z - h.pointA.z;
+        ta[t] = f4(h.pointA.x, h.pointA.y, h.pointA.z, e1x);
+        tb[t] = f4(e1y, e1z, e2x, e2y);
+        tc[t] = e2z;
+        nrm[3 * t] = f4(h.normalA.x, h.normalA.y, h.normalA.z, 0.0f);
+        nrm[3 * t + 1] = f4(h.normalB.x - h.normalA.x, h.normalB.y - h.normalA.y, h.normalB.z - h.normalA.z, 0.0f);
+        nrm[3 * t + 2] = f4(h.normalC.x - h.normalA.x, h.normalC.y - h.normalA.y, h.normalC.z - h.normalA.z, 0.0f);
+    }
+    // ---- BLAS: validate every mesh's tree by DFS and build child-pair records + leaf table
+    std::vector<float4> rec(size_t(n_nodes) * 4, f4(0, 0, 0, 0));
+    std::vector<uint2> leaf(size_t(n_nodes), make_uint2(0, 0));
+    std::vector<int64_t> owner(size_t(n_nodes), -1);  // (accOffset << 32 | triOffset) that produced the entry
+    std::vector<HgDevMesh> dm(static_cast<size_t>(n_meshes));
+    uint32_t max_depth = 0;
+    auto ref_of = [&](uint32_t g) { return g | (blas[g].triangleCount > 0 ? HG_LEAF_BIT : 0u); };
+    std::vector<std::pair<uint32_t, uint32_t>> dfs;
+    for (int mi = 0; mi < n_meshes; ++mi) {
+        const HalogenMeshData& m = meshes[mi];
+        if (m.materialIndex >= uint32_t(n_materials))
+            return fail(c, HG_E_INVALID, "mesh %d: materialIndex %u out of range", mi, m.materialIndex);
+        const uint32_t off = m.accelerationBufferOffset, toff = m.triangleBufferOffset;
+        if (off >= uint32_t(n_nodes)) return fail(c, HG_E_INVALID, "mesh %d: accelerationBufferOffset out of range", mi);
+        const int64_t key = (int64_t(off) << 32) | int64_t(toff);
+        dfs.assign(1, {off, 0u});
+        while (!dfs.empty()) {
+            auto [g, depth] = dfs.back();
+            dfs.pop_back();
+            if (depth + 2 > kMaxStack)
+                return fail(c, HG_E_UNSUPPORTED, "mesh %d: BLAS deeper than %u levels (or cyclic)", mi, kMaxStack - 2);
+            max_depth = std::max(max_depth, depth);
+            if (owner[g] != -1 && owner[g] != key)
+                return fail(c, HG_E_UNSUPPORTED, "BLAS entry %u shared by meshes with different offsets", g);
+            owner[g] = key;
+            const BVHEntry& e = blas[g];
+            if (e.triangleCount > 0) {
+                if (uint64_t(toff) + e.indexA + e.triangleCount > uint64_t(n_tris))
+                    return fail(c, HG_E_INVALID, "mesh %d: leaf %u references triangles out of range", mi, g);
+                leaf[g] = make_uint2(toff + e.indexA, e.triangleCount);
+            } else {
+                const uint64_t a = uint64_t(off) + e.indexA;
+                if (a + 1 >= uint64_t(n_nodes))
+                    return fail(c, HG_E_INVALID, "mesh %d: node %u has children out of range", mi, g);
+                const BVHEntry& A = blas[a];
+                const BVHEntry& B = blas[a + 1];
+                rec[4 * size_t(g)] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z,
+                                       bits(ref_of(uint32_t(a))));
+                rec[4 * size_t(g) + 1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z,
+                                           bits(ref_of(uint32_t(a + 1))));
+                rec[4 * size_t(g) + 2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
+                rec[4 * size_t(g) + 3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
+                dfs.push_back({uint32_t(a + 1), depth + 1});
+                dfs.push_back({uint32_t(a), depth + 1});
+            }
+        }
+        std::memcpy(dm[mi].w2l, m.worldToLocal.m, sizeof dm[mi].w2l);
+        dm[mi].root_ref = ref_of(off);
+        dm[mi].tri_offset = toff;
+        dm[mi].material = m.materialIndex;
+        dm[mi].pad = 0;
+    }
+    c->stack_depth = std::max<uint32_t>(2u, (max_depth + 2 + 1) & ~1u);
+
+    int rc;
+    if ((rc = upload(c, c->spheres, sph.data(), sph.size() * sizeof(float4)))) return rc;
+    if ((rc = upload(c, c->materials, mat.data(), mat.size() * sizeof(float4)))) return rc;
+    if ((rc = upload(c, c->meshes, dm.data(), dm.size() * sizeof(HgDevMesh)))) return rc;
+    if ((rc = upload(c, c->nodes, rec.data(), rec.size() * sizeof(float4)))) return rc;
+    if ((rc = upload(c, c->leaves, leaf.data(), leaf.size() * sizeof(uint2)))) return rc;
+    if ((rc = upload(c, c->tri_a, ta.data(), ta.size() * sizeof(float4)))) return rc;
+    if ((rc = upload(c, c->tri_b, tb.data(), tb.size() * sizeof(float4)))) return rc;
+    if ((rc = upload(c, c->tri_c, tc.data(), tc.size() * sizeof(float)))) return rc;
+    if ((rc = upload(c, c->normals, nrm.data(), nrm.size() * sizeof(float4)))) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));  // host staging vectors die at return
+    c->n_spheres = n_spheres;
+    c->n_meshes = n_meshes;
+    c->n_materials = n_materials;
+    c->n_tris = n_tris;
+    c->n_nodes = n_nodes;
+    c->has_scene = true;
+    return HG_OK;
+}
+
+int hg_upload_cubemap(hg_ctx* c, int32_t face_size, int32_t n_mips, const float* texels, size_t n_floats) {
+    if (!c) return HG_E_INVALID;
+    if (face_size <= 0 || n_mips <= 0 || n_mips > HG_MAX_CUBE_MIPS || !texels)
+        return fail(c, HG_E_INVALID, "bad cubemap shape");
+    uint64_t need = 0;
+    for (int m = 0; m < n_mips; ++m) {
+        c->cube_mip_offset[m] = uint32_t(need / 4);
+        const uint64_t s = std::max(1, face_size >> m);
+        need += 6ull * s * s * 4ull;
+    }
+    if (need != n_floats) return fail(c, HG_E_INVALID, "cubemap has %zu floats, expected %llu", n_floats,
+                                      (unsigned long long)need);
+    if (int rc = set_device(c)) return rc;
+    if (int rc = upload(c, c->cube, texels, n_floats * sizeof(float))) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    c->cube_size = face_size;
+    c->cube_mips = n_mips;
+    return HG_OK;
+}
+
+int hg_set_params(hg_ctx* c, const hg_params* p) {
+    if (!c || !p) return HG_E_INVALID;
+    if (p->samplesPerPixel < 1) return fail(c, HG_E_INVALID, "samplesPerPixel must be >= 1");
+    if (!(p->screenParameters.x >= 1.0f) || !(p->screenParameters.y >= 1.0f))
+        return fail(c, HG_E_INVALID, "screenParameters must be >= 1");
+    c->params = *p;
+    c->has_params = true;
+    return HG_OK;
+}
+
+int hg_resize(hg_ctx* c, int32_t width, int32_t height) {
+    if (!c) return HG_E_INVALID;
+    if (width <= 0 || height <= 0 || int64_t(width) * height > (int64_t(1) << 31))
+        return fail(c, HG_E_INVALID, "bad target size %dx%d", width, height);
+    if (int rc = set_device(c)) return rc;
+    c->W = width;
+    c->H = height;
+    return alloc_target(c);
+}
+
+int hg_set_tiling(hg_ctx* c, int32_t rank, int32_t n_ranks) {
+    if (!c) return HG_E_INVALID;
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(c, HG_E_INVALID, "bad tiling %d/%d", rank, n_ranks);
+    if (int rc = set_device(c)) return rc;
+    c->rank = rank;
+    c->n_ranks = n_ranks;
+    return c->W > 0 ? alloc_target(c) : HG_OK;
+}
+
+int hg_clear_accumulation(hg_ctx* c) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = set_device(c)) return rc;
+    if (c->acc.p) HG_HIP(c, hipMemsetAsync(c->acc.p, 0, c->acc.bytes, c->stream));
+    return HG_OK;
+}
+
+int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
+    if (!c) return HG_E_INVALID;
+    if (!c->has_scene) return fail(c, HG_E_NOSCENE, "hg_upload_scene not called");
+    if (!c->has_params) return fail(c, HG_E_INVALID, "hg_set_params not called");
+    if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
+    if (n_frames < 0) return fail(c, HG_E_INVALID, "n_frames < 0");
+    const hg_params& p = c->params;
+    if (int32_t(p.screenParameters.x) != c->W || int32_t(p.screenParameters.y) != c->H)
+        return fail(c, HG_E_INVALID, "screenParameters (%g,%g) != target %dx%d", p.screenParameters.x,
+                    p.screenParameters.y, c->W, c->H);
+    const int32_t ns = int32_t(p.bufferCounts.x), nm = int32_t(p.bufferCounts.y);
+    if (ns < 0 || ns > c->n_spheres || nm < 0 || nm > c->n_meshes)
+        return fail(c, HG_E_INVALID, "bufferCounts (%d,%d) exceed uploaded (%d,%d)", ns, nm, c->n_spheres, c->n_meshes);
+    if (n_frames == 0) return HG_OK;
+    if (int rc = set_device(c)) return rc;
+
+    HgKernelParams kp{};
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 4; ++k) kp.cam[r * 4 + k] = p.camLocalToWorld.m[k * 4 + r];
+    kp.W = p.screenParameters.x;
+    kp.H = p.screenParameters.y;
+    kp.Wu = uint32_t(p.screenParameters.x);
+    kp.Hu = uint32_t(c->H);
+    kp.vw = p.viewParameters.x;
+    kp.vh = p.viewParameters.y;
+    kp.near_ = p.viewParameters.z;
+    kp.far_ = p.viewParameters.w;
+    // tan(radians(focalConeAngle)) * ViewParameters.z (:998), once per launch with the shared spec
+    kp.focal_disc_radius = hg_tanf(p.focalConeAngle * HG_DEG2RAD) * p.viewParameters.z;
+    kp.psx = (p.viewParameters.x * 2.0f) / p.screenParameters.x;  // get_ray_jitter :986
+    kp.psy = (p.viewParameters.y * 2.0f) / p.screenParameters.y;
+    kp.filter_radius = p.filterRadius;
+    kp.focal_dist = p.focalPlaneDistance;
+    kp.spp = p.samplesPerPixel;
+    kp.max_bounces = p.maxBounces;
+    kp.max_diff = p.maxDiffuseBounces;
+    kp.max_glossy = p.maxGlossyBounces;
+    kp.max_trans = p.maxTransmissionBounces;
+    kp.debug_mode = p.halogenDebugMode;
+    kp.tri_range = p.triangleDebugDisplayRange;
+    kp.box_range = p.boxDebugDisplayRange;
+    kp.default_mip = p.defaultHDRIMipLevel;
+    kp.use_cube = (p.useEnvironmentCubemap > 0 && c->cube_mips > 0) ? 1 : 0;
+    kp.n_spheres = ns;
+    kp.n_meshes = nm;
+    kp.first_frame = accumulate ? p.frameCount : 1;
+    kp.n_frames = n_frames;
+    kp.accumulate = accumulate ? 1 : 0;
+    kp.tiles_x = c->tiles_x;
+    kp.rank = c->rank;
+    kp.n_ranks = c->n_ranks;
+    kp.n_local_tiles = c->n_local_tiles;
+    kp.stack_depth = c->stack_depth;
+    kp.cube_size = c->cube_size;
+    kp.cube_mips = c->cube_mips;
+    std::memcpy(kp.cube_mip_offset, c->cube_mip_offset, sizeof kp.cube_mip_offset);
+    kp.spheres = static_cast<const float4*>(c->spheres.p);
+    kp.meshes = static_cast<const HgDevMesh*>(c->meshes.p);
+    kp.materials = static_cast<const float4*>(c->materials.p);
+    kp.nodes = static_cast<const float4*>(c->nodes.p);
+    kp.leaves = static_cast<const uint2*>(c->leaves.p);
+    kp.tri_a = static_cast<const float4*>(c->tri_a.p);
+    kp.tri_b = static_cast<const float4*>(c->tri_b.p);
+    kp.tri_c = static_cast<const float*>(c->tri_c.p);
+    kp.normals = static_cast<const float4*>(c->normals.p);
+    kp.cube = static_cast<const float4*>(c->cube.p);
+    kp.acc = static_cast<float4*>(c->acc.p);
+    kp.counters = static_cast<unsigned long long*>(c->counters_dev.p);
+
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (!c->free_events.empty()) {
+        ev = c->free_events.back();
+        c->free_events.pop_back();
+    } else {
+        HG_HIP(c, hipEventCreate(&ev.first));
+        HG_HIP(c, hipEventCreate(&ev.second));
+    }
+    HG_HIP(c, hipEventRecord(ev.first, c->stream));
+    hipError_t e = hg_launch_trace(kp, c->block, c->counters_on != 0, c->stream);
+    if (e != hipSuccess) {
+        c->free_events.push_back(ev);
+        return fail(c, HG_E_HIP, "trace kernel launch failed: %s", hipGetErrorString(e));
+    }
+    HG_HIP(c, hipEventRecord(ev.second, c->stream));
+    c->pending.push_back(ev);
+    c->counters.launches++;
+    if (c->pending.size() > 256) {
+        if (int rc = drain_events(c)) return rc;
+    }
+    if (accumulate) c->params.frameCount += n_frames;  // FrameCount++ per accumulated frame (RP:347)
+    return HG_OK;
+}
+
+int hg_synchronize(hg_ctx* c) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = set_device(c)) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    return drain_events(c);
+}
+
+int32_t hg_local_tile_count(const hg_ctx* c) { return c ? c->n_local_tiles : 0; }
+
+int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
+    if (!c || !rgba) return HG_E_INVALID;
+    if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
+    if (n_floats < size_t(c->W) * size_t(c->H) * 4) return fail(c, HG_E_INVALID, "readback buffer too small");
+    if (int rc = set_device(c)) return rc;
+    std::vector<float4> tiles(size_t(c->n_local_tiles) * 64);
+    if (!tiles.empty())
+        HG_HIP(c, hipMemcpyAsync(tiles.data(), c->acc.p, tiles.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc = drain_events(c)) return rc;
+    for (int32_t lt = 0; lt < c->n_local_tiles; ++lt) {
+        const int64_t gt = int64_t(c->rank) + int64_t(lt) * c->n_ranks;
+        const int tx = int(gt % c->tiles_x), ty = int(gt / c->tiles_x);
+        for (int l = 0; l < 64; ++l) {
+            const int x = tx * HG_TILE + (l & 7), y = ty * HG_TILE + (l >> 3);
+            if (x >= c->W || y >= c->H) continue;
+            const float4 v = tiles[size_t(lt) * 64 + l];
+            float* d = rgba + (size_t(y) * c->W + x) * 4;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    }
+    return HG_OK;
+}
+
+int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
+    if (!c || !dst) return HG_E_INVALID;
+    const size_t need = size_t(c->n_local_tiles) * 64 * sizeof(float4);
+    if (n_bytes < need) return fail(c, HG_E_INVALID, "destination too small (%zu < %zu)", n_bytes, need);
+    if (int rc = set_device(c)) return rc;
+    if (need) HG_HIP(c, hipMemcpyAsync(dst, c->acc.p, need, hipMemcpyDeviceToDevice, c->stream));
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    return drain_events(c);
+}
+
+int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
+    hg_ctx* c = const_cast<hg_ctx*>(cc);
+    if (!c || !out) return HG_E_INVALID;
+    if (int rc = set_device(c)) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc = drain_events(c)) return rc;
+    unsigned long long v[16];
+    HG_HIP(c, hipMemcpy(v, c->counters_dev.p, sizeof v, hipMemcpyDeviceToHost));
+    *out = c->counters;
+    out->paths = v[0];
+    out->rays = v[1];
+    out->tri_tests = v[2];
+    out->aabb_tests = v[3];
+    out->mesh_visits = v[4];
+    out->sphere_tests = v[5];
+    out->hits = v[6];
+    return HG_OK;
+}
+
+int hg_reset_counters(hg_ctx* c) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = set_device(c)) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc = drain_events(c)) return rc;
+    HG_HIP(c, hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes));
+    c->counters = hg_counters{};
+    return HG_OK;
+}
+
+int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
+    if (!c) return HG_E_INVALID;
+    switch (option) {
+        case HG_OPT_KERNEL:
+            if (value != HG_KERNEL_MEGA) return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
+            c->kernel = value;
+            return HG_OK;
+        case HG_OPT_BLOCK:
+            if (value != 64 && value != 128 && value != 256) return fail(c, HG_E_INVALID, "block must be 64/128/256");
+            c->block = value;
+            return HG_OK;
+        case HG_OPT_COUNTERS:
+            c->counters_on = value ? 1 : 0;
+            return HG_OK;
+        default:
+            return fail(c, HG_E_INVALID, "unknown option %d", option);
+    }
+}
+
+}  // extern "C"

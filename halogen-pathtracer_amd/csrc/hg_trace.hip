@@ -1,0 +1,714 @@
+// hg_trace.hip — the Halogen path-tracing megakernel for gfx950 (CDNA4, wave64).
+//
+// Reference: Assets/Scripts/Halogen Shaders/HalgoenCompute.compute (kernel HalogenCompute, :1015-1063)
+//            Assets/Scripts/Halogen Shaders/HalogenRandom.hlsl   (sampler)
+//            Assets/Scripts/Halogen Shaders/AccumulationShader.shader:27-34 (fused here as the epilogue)
+//
+// Execution model (MI355X-first, not a translation of the [numthreads(8,8,1)] HLSL dispatch):
+//   * one wave64 = one 8x8 pixel tile; a 256-thread workgroup = 4 tiles.  Tiles are dealt to ranks
+//     round-robin (multi-GPU) and the accumulation buffer is tile-major, so each wave reads and writes
+//     one contiguous KiB of float4.
+//   * each lane runs n_frames frames of its pixel back to back (FrameCount = first .. first+n-1) and
+//     keeps the progressive average in registers: the accumulation "blit" of the reference becomes the
+//     kernel epilogue, and the 16-B accumulator crosses HBM once per launch instead of 3x per frame.
+//   * BLAS traversal uses a per-lane stack in LDS laid out [depth][lane] (lane-contiguous, conflict-free
+//     ds_read/write_b32), child-pair node records (hg_layout.h) and pre-subtracted triangle edges.
+//   * the Owen-scrambled Sobol sampler uses closed forms of the two Sobol dimensions the reference uses:
+//     sobol(i, 0) = bitreverse(i) and sobol(i, 1) = bitreverse(superset-XOR-transform(i)), so
+//     owen_scramble(sobol(i,d), s) = bitreverse(LK(·, s)) needs no 32-iteration loop; bit-exact with
+//     the reference's table loop (tests/test_sampler_closed_form.py, and the GPU parity tests).
+//   * all fp arithmetic follows the reference's operation order with -ffp-contract=off and the shared
+//     spec include/hg_fmath.h, so results are bit-identical to the CPU oracle.
+//   * per-lane work counters (TriangleTests / AABBTests of the reference, rays, hits) are reduced per
+//     wave with DPP/permute shuffles and added with one 64-bit atomic per wave per counter.
+#include <hip/hip_runtime.h>
+
+#include "hg_fmath.h"
+#include "hg_layout.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------------
+// float3 helpers with the reference's evaluation order (no FMA)
+// ---------------------------------------------------------------------------------------------------
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 a) { return a * hg_rnorm(dot(a, a)); }
+__device__ __forceinline__ f3 lerp(f3 a, f3 b, float s) { return a + (b - a) * s; }
+__device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
+
+// mul(M, float4(v, w)), M given row-major in m[r*4+c] (rows 0..2)
+__device__ __forceinline__ f3 xform(const float* m, f3 v, float w) {
+    return mk(((m[0] * v.x + m[1] * v.y) + m[2] * v.z) + m[3] * w,
+              ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * w,
+              ((m[8] * v.x + m[9] * v.y) + m[10] * v.z) + m[11] * w);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Sampler (HalogenRandom.hlsl)
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {  // u32_hash :110-115
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+__device__ __forceinline__ uint32_t hash_combine(uint32_t seed, uint32_t v) {  // :131-133
+    return seed ^ (v + (seed << 6) + (seed >> 2));
+}
+// the Laine–Karras-style body of owen_scramble (:154-158), on the already bit-reversed value
+__device__ __forceinline__ uint32_t lk_body(uint32_t x, uint32_t seed) {
+    x ^= x * 0x3d20adeau;
+    x += seed;
+    x *= (seed >> 16) | 1u;
+    x ^= x * 0x05526c56u;
+    x ^= x * 0x53a22864u;
+    return x;
+}
+__device__ __forceinline__ uint32_t brev(uint32_t x) { return __builtin_bitreverse32(x); }
+// owen_scramble(v, s) = brev(lk(brev(v), s))
+__device__ __forceinline__ uint32_t owen(uint32_t v, uint32_t s) { return brev(lk_body(brev(v), s)); }
+// Sobol dimension 1 (Pascal matrix mod 2): bit p (MSB-first) of sobol(i,1) = XOR over set bits k of i
+// with k ⊇ p  ->  superset-XOR transform of i, then bit-reversed.
+__device__ __forceinline__ uint32_t superset_xor(uint32_t z) {
+    z ^= (z >> 1) & 0x55555555u;
+    z ^= (z >> 2) & 0x33333333u;
+    z ^= (z >> 4) & 0x0F0F0F0Fu;
+    z ^= (z >> 8) & 0x00FF00FFu;
+    z ^= (z >> 16) & 0x0000FFFFu;
+    return z;
+}
+constexpr float kInv2_32 = 4294967296.0f;
+
+struct Sampler {
+    uint32_t frame;   // Sobol index (FrameCount)
+    uint32_t pixel;   // pixelID = u32_hash(x + y*W)
+    uint32_t offset;  // SobolDimensionOffset
+    // float_owen_scrambled_sobol (:252-259): owen(sobol(i,0), pcg(seed)) = brev(lk(i, pcg(seed)))
+    __device__ __forceinline__ float get1(uint32_t id) const {
+        uint32_t seed = pixel ^ pcg_hash(offset + id);
+        return float(brev(lk_body(frame, pcg_hash(seed)))) / kInv2_32;
+    }
+    // float2_owen_scrambled_sobol (:261-268, :215-228)
+    __device__ __forceinline__ void get2(uint32_t id, float& a, float& b) const {
+        uint32_t seed = pixel ^ pcg_hash(offset + id);
+        uint32_t sh = owen(frame, seed);  // shuffled index
+        a = float(brev(lk_body(sh, hash_combine(seed, 0u)))) / kInv2_32;
+        b = float(brev(lk_body(superset_xor(sh), hash_combine(seed, 1u)))) / kInv2_32;
+    }
+};
+
+constexpr uint32_t ID_FOCAL = 0, ID_JITTER = 1, ID_ROUGH = 2, ID_PROPERTY = 3, ID_RR = 4, BOUNCE_INC = 5;
+#define HLSL_PI (180.0f * HG_DEG2RAD)
+
+// ---------------------------------------------------------------------------------------------------
+// Per-lane path state
+// ---------------------------------------------------------------------------------------------------
+struct Counters {
+    uint32_t rays, tri, aabb, meshes, spheres, hits;
+};
+
+// bounceTypes[3] of trace_ray (:887) kept as three named registers (a runtime-indexed array would go to
+// scratch memory on gfx950)
+struct Bounces {
+    uint32_t diffuse, glossy, transmission;
+    __device__ __forceinline__ void bump(uint32_t t) {
+        diffuse += t == 0u;
+        glossy += t == 1u;
+        transmission += t == 2u;
+    }
+};
+
+struct Ray {
+    f3 o, d;
+};
+
+struct Hit {
+    float t;
+    float orient;
+    f3 pos, n;
+    uint32_t mat;
+};
+
+// nested-dielectric stack (:188-189): 8 material indices packed one byte each in a u64 (the medium of a
+// stack entry is always the internal medium of a material, so its index identifies it completely)
+struct MediumStack {
+    uint64_t s;
+    int sp;
+    __device__ __forceinline__ uint32_t get(int i) const { return uint32_t(s >> (8 * i)) & 0xFFu; }
+};
+
+// material record accessors
+struct Mat {
+    float4 albedo, spec_metal, emis_rough, absorb_ior, prio_id_r2;
+};
+__device__ __forceinline__ Mat load_mat(const HgKernelParams& kp, uint32_t m) {
+    const float4* p = kp.materials + 5 * m;
+    return Mat{p[0], p[1], p[2], p[3], p[4]};
+}
+__device__ __forceinline__ int32_t mat_priority(const HgKernelParams& kp, uint32_t m) {
+    return __float_as_int(kp.materials[5 * m + 4].x);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Intersection (:244-485)
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-259
+    f3 t1 = (A - o) * inv;
+    f3 t2 = (B - o) * inv;
+    float tMin = fminf(t1.x, t2.x);
+    float tMax = fmaxf(t1.x, t2.x);
+    tMin = fmaxf(tMin, fminf(t1.y, t2.y));
+    tMax = fminf(tMax, fmaxf(t1.y, t2.y));
+    tMin = fmaxf(tMin, fminf(t1.z, t2.z));
+    tMax = fminf(tMax, fmaxf(t1.z, t2.z));
+    return tMax > fmaxf(0.0f, tMin) ? tMin : HG_INF;
+}
+
+__device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c) {  // :357-376
+    float closest = h.t;
+    f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    for (int i = 0; i < kp.n_spheres; ++i) {
+        const float4 cr = kp.spheres[3 * i];
+        const float4 am = kp.spheres[3 * i + 1];
+        const float4 b = kp.spheres[3 * i + 2];
+        c.spheres++;
+        if (!(ray_aabb(xyz(am), xyz(b), ray.o, inv) < kp.far_)) continue;
+        // sphere_intersection :266-303
+        f3 center = xyz(cr);
+        f3 sh = ray.o - center;
+        float bq = 2.0f * dot(sh, ray.d);
+        float cq = dot(sh, sh) - cr.w * cr.w;
+        float disc = bq * bq - 4.0f * cq;
+        if (!(disc >= 0.0f)) continue;  // rayT = INF: never accepted
+        float hd = (-bq - __builtin_sqrtf(disc)) / 2.0f;
+        float orient = 1.0f;
+        if (hd < 0.0f) {
+            hd = (-bq + __builtin_sqrtf(disc)) / 2.0f;
+            orient = -1.0f;
+        }
+        if (hd < closest && hd > 0.0001f) {
+            h.t = hd;
+            h.orient = orient;
+            h.pos = ray.o + ray.d * hd;
+            h.n = normalize(h.pos - center) * orient;
+            h.mat = __float_as_uint(am.w);
+            closest = hd;
+        }
+    }
+}
+
+// get_ray_scene_intersection_mesh, :378-472.  `stack` points at this lane's column of the LDS stack.
+__device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, uint32_t* stack,
+                             uint32_t stride) {
+    const float eps = 0.0001f;
+    float best_t = h.t;  // closestIntersection.rayT starts at the sphere hit (:381)
+    float best_u = 0.0f, best_v = 0.0f, best_o = 0.0f;
+    uint32_t best_tri = 0xFFFFFFFFu;  // global triangle index
+    int best_mesh = -1;
+    for (int mi = 0; mi < kp.n_meshes; ++mi) {
+        const HgDevMesh& md = kp.meshes[mi];
+        c.meshes++;
+        // world -> local, direction NOT normalized (:390-392); md.w2l is Unity column-major: M(r,c)=w2l[c*4+r]
+        const float* m = md.w2l;
+        f3 lo = mk(((m[0] * ray.o.x + m[4] * ray.o.y) + m[8] * ray.o.z) + m[12] * 1.0f,
+                   ((m[1] * ray.o.x + m[5] * ray.o.y) + m[9] * ray.o.z) + m[13] * 1.0f,
+                   ((m[2] * ray.o.x + m[6] * ray.o.y) + m[10] * ray.o.z) + m[14] * 1.0f);
+        f3 ld = mk(((m[0] * ray.d.x + m[4] * ray.d.y) + m[8] * ray.d.z) + m[12] * 0.0f,
+                   ((m[1] * ray.d.x + m[5] * ray.d.y) + m[9] * ray.d.z) + m[13] * 0.0f,
+                   ((m[2] * ray.d.x + m[6] * ray.d.y) + m[10] * ray.d.z) + m[14] * 0.0f);
+        f3 inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+        uint32_t sp = 0;
+        stack[0] = md.root_ref;  // root pushed untested (:401)
+        sp = 1;
+        while (sp > 0) {
+            const uint32_t ref = stack[(--sp) * stride];
+            if (ref & HG_LEAF_BIT) {
+                const uint2 leaf = kp.leaves[ref & ~HG_LEAF_BIT];
+                for (uint32_t k = 0; k < leaf.y; ++k) {
+                    const uint32_t ti = leaf.x + k;
+                    const float4 ta = kp.tri_a[ti];
+                    const float4 tb = kp.tri_b[ti];
+                    const float tc = kp.tri_c[ti];
+                    c.tri++;
+                    // triangle_intersection_doublesided :307-355
+                    const f3 e1 = mk(ta.w, tb.x, tb.y);
+                    const f3 e2 = mk(tb.z, tb.w, tc);
+                    const f3 pvec = cross(ld, e2);
+                    const float det = dot(pvec, e1);
+                    if (fabsf(det) < 0.00000001f) continue;
+                    const float inv_det = 1.0f / det;
+                    const f3 tvec = lo - xyz(ta);
+                    const float U = dot(tvec, pvec) * inv_det;
+                    if (U < 0.0f || U > 1.0f) continue;
+                    const f3 qvec = cross(tvec, e1);
+                    const float V = dot(ld, qvec) * inv_det;
+                    if (V < 0.0f || U + V > 1.0f) continue;
+                    const float t = dot(e2, qvec) * inv_det;
+                    if (!(t > 0.0f)) continue;
+                    if (t > eps && t < best_t) {
+                        best_t = t;
+                        best_u = U;
+                        best_v = V;
+                        best_o = det > 0.0f ? 1.0f : -1.0f;
+                        best_tri = ti;
+                        best_mesh = mi;
+                    }
+                }
+            } else {
+                const float4* rec = kp.nodes + 4 * (ref);
+                const float4 a_lo = rec[0], a_hi = rec[1], b_lo = rec[2], b_hi = rec[3];
+                const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
+                const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                c.aabb += 2;
+                const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                // push the farther child first so the nearer is popped first (:430-444)
+                if (dB < dA) {
+                    if (dA < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refA;
+                    if (dB < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refB;
+                } else {
+                    if (dB < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refB;
+                    if (dA < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refA;
+                }
+            }
+        }
+    }
+    // :452-471
+    if (best_t < (h.t - eps) && best_t < kp.far_) {
+        const HgDevMesh& md = kp.meshes[best_mesh];
+        h.t = best_t;
+        h.mat = md.material;
+        h.orient = best_o;
+        const float4 n0 = kp.normals[3 * best_tri], d1 = kp.normals[3 * best_tri + 1],
+                     d2 = kp.normals[3 * best_tri + 2];
+        f3 n = (xyz(n0) + xyz(d1) * best_u) + xyz(d2) * best_v;
+        n = n * best_o;
+        // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform)
+        const float* m = md.w2l;
+        f3 w = mk(((n.x * m[0] + n.y * m[1]) + n.z * m[2]) + 0.0f * m[3],
+                  ((n.x * m[4] + n.y * m[5]) + n.z * m[6]) + 0.0f * m[7],
+                  ((n.x * m[8] + n.y * m[9]) + n.z * m[10]) + 0.0f * m[11]);
+        h.n = normalize(w);
+        h.pos = ray.o + ray.d * best_t;
+    }
+}
+
+__device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ray, Counters& c, uint32_t* stack,
+                                         uint32_t stride) {  // get_ray_intersection :474-485
+    Hit h;
+    h.t = HG_INF;
+    h.orient = 0.0f;
+    h.pos = mk(0, 0, 0);
+    h.n = mk(0, 0, 0);
+    h.mat = 0;
+    c.rays++;
+    isect_spheres(kp, ray, h, c);
+    isect_meshes(kp, ray, h, c, stack, stride);
+    return h;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Sky (:196-204) — manual bilinear cubemap, the build's definition of SampleLevel
+// ---------------------------------------------------------------------------------------------------
+__device__ f3 sample_sky(const HgKernelParams& kp, f3 dir, int level) {
+    if (!(kp.use_cube > 0)) return mk(0, 0, 0);
+    float x = dir.x, y = dir.y, z = dir.z;
+    float ax = fabsf(x), ay = fabsf(y), az = fabsf(z);
+    int face;
+    float sc, tc, ma;
+    if (az >= ax && az >= ay) {
+        ma = az;
+        if (z >= 0) { face = 4; sc = x; tc = -y; } else { face = 5; sc = -x; tc = -y; }
+    } else if (ay >= ax) {
+        ma = ay;
+        if (y >= 0) { face = 2; sc = x; tc = z; } else { face = 3; sc = x; tc = -z; }
+    } else {
+        ma = ax;
+        if (x >= 0) { face = 0; sc = -z; tc = -y; } else { face = 1; sc = z; tc = -y; }
+    }
+    level = level < 0 ? 0 : (level > kp.cube_mips - 1 ? kp.cube_mips - 1 : level);
+    int size = kp.cube_size >> level;
+    size = size < 1 ? 1 : size;
+    const float4* tex = kp.cube + kp.cube_mip_offset[level] + size_t(face) * size * size;
+    float s = (sc / ma + 1.0f) * 0.5f;
+    float t = (tc / ma + 1.0f) * 0.5f;
+    float u = s * float(size) - 0.5f, v = t * float(size) - 0.5f;
+    float fu = floorf(u), fv = floorf(v);
+    float fx = u - fu, fy = v - fv;
+    int x0 = int(fu), y0 = int(fv);
+    int x1 = x0 + 1, y1 = y0 + 1;
+    x0 = min(max(x0, 0), size - 1);
+    x1 = min(max(x1, 0), size - 1);
+    y0 = min(max(y0, 0), size - 1);
+    y1 = min(max(y1, 0), size - 1);
+    const float4 c00 = tex[y0 * size + x0], c10 = tex[y0 * size + x1];
+    const float4 c01 = tex[y1 * size + x0], c11 = tex[y1 * size + x1];
+    const float gx = 1.0f - fx, gy = 1.0f - fy;
+    f3 top = xyz(c00) * gx + xyz(c10) * fx;
+    f3 bot = xyz(c01) * gx + xyz(c11) * fx;
+    return top * gy + bot * fy;
+}
+
+__device__ __forceinline__ int sky_level(const HgKernelParams& kp, float acc_rough) {
+    float lf = hg_roundf(float(kp.default_mip) + acc_rough * 8.0f);
+    if (!(lf >= 0.0f)) return 0;
+    if (lf > 64.0f) return 64;
+    return int(lf);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// BSDF (:491-741) and medium stack (:582-665)
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f3 lambert(f3 n, f3 rv) {  // :491-501
+    f3 p = rv + n;
+    if (len(p) < 1e-8f) p = n;
+    return normalize(p);
+}
+__device__ __forceinline__ f3 reflect(f3 i, f3 n) { return i - n * (2.0f * dot(i, n)); }  // :506-509
+
+__device__ __forceinline__ float schlick_adjusted(float n1, float n2, f3 nrm, f3 inc, float mn, float mx) {
+    float r0 = (n1 - n2) / (n1 + n2);  // :519-540
+    r0 *= r0;
+    float cosX = -dot(nrm, inc);
+    if (n1 > n2) {
+        float n = n1 / n2;
+        float sinT2 = n * n * (1.0f - cosX * cosX);
+        if (sinT2 > 1.0f) return mx;
+        cosX = __builtin_sqrtf(1.0f - sinT2);
+    }
+    float x = 1.0f - cosX;
+    float ret = r0 + (1.0f - r0) * x * x * x * x * x;
+    return mn + ret * (mx - mn);
+}
+
+__device__ __forceinline__ f3 refract_tir(f3 inc, f3 nrm, float n1, float n2, bool& tir) {  // :557-572
+    float ct = fminf(dot(-inc, nrm), 1.0f);
+    float st = __builtin_sqrtf(1.0f - ct * ct);
+    float n12 = n1 / n2;
+    if (n12 * st > 1.0f) {
+        tir = true;
+        return reflect(inc, nrm);
+    }
+    f3 perp = (inc + nrm * ct) * n12;
+    float lp = len(perp);
+    f3 par = nrm * (-__builtin_sqrtf(fabsf(1.0f - lp * lp)));
+    return perp + par;
+}
+
+struct Medium {
+    float ior;
+    f3 absorb;
+    uint32_t id;
+};
+__device__ __forceinline__ Medium medium_of(const HgKernelParams& kp, uint32_t m) {
+    const float4 ai = kp.materials[5 * m + 3];
+    const float4 pr = kp.materials[5 * m + 4];
+    return Medium{ai.w, xyz(ai), __float_as_uint(pr.y)};
+}
+__device__ __forceinline__ Medium empty_medium() { return Medium{1.0f, mk(0, 0, 0), 0xFFFFFFFFu}; }
+__device__ __forceinline__ Medium top_medium(const HgKernelParams& kp, const MediumStack& ms) {
+    return ms.sp > 0 ? medium_of(kp, ms.get(ms.sp - 1)) : empty_medium();
+}
+__device__ void medium_push(const HgKernelParams& kp, MediumStack& ms, uint32_t m) {  // :582-622
+    if (ms.sp == 0) {
+        ms.s = uint64_t(m);
+        ms.sp = 1;
+        return;
+    }
+    const int32_t prio = mat_priority(kp, m);
+    int ins = ms.sp;
+    if (prio > mat_priority(kp, ms.get(ms.sp - 1))) {
+        for (int i = ms.sp - 1; i >= 0; --i) {
+            if (prio < mat_priority(kp, ms.get(i))) {
+                ins = i + 1;
+                break;
+            }
+        }
+        if (ins == ms.sp) ins = 0;
+    }
+    if (ms.sp >= 8) return;  // overflow: dropped (reference UB; same rule in the oracle)
+    const uint64_t low_mask = ins == 0 ? 0ull : (~0ull >> (64 - 8 * ins));
+    const uint64_t low = ms.s & low_mask;
+    const uint64_t high = ms.s & ~low_mask;
+    ms.s = low | (high << 8) | (uint64_t(m) << (8 * ins));
+    ms.sp++;
+}
+__device__ void medium_pop(const HgKernelParams& kp, MediumStack& ms, uint32_t id) {  // :627-642
+    for (int i = 0; i < ms.sp; ++i) {
+        if (medium_of(kp, ms.get(i)).id == id) {
+            const uint64_t low_mask = i == 0 ? 0ull : (~0ull >> (64 - 8 * i));
+            const uint64_t low = ms.s & low_mask;
+            const uint64_t high = (i + 1 < 8) ? ((ms.s >> (8 * (i + 1))) << (8 * i)) : 0ull;
+            ms.s = low | high;
+            ms.sp--;
+            return;
+        }
+    }
+}
+
+// material_BRDF :672-741
+__device__ f3 material_brdf(const HgKernelParams& kp, const Sampler& smp, Ray& ray, const Hit& hit, const Mat& mt,
+                            const Medium& cur, const Medium& hm, uint32_t& bt) {
+    f3 att;
+    float rr0, rr1, pr0, pr1;
+    smp.get2(ID_ROUGH, rr0, rr1);
+    smp.get2(ID_PROPERTY, pr0, pr1);
+    // get_random_unit_vector (HalogenRandom.hlsl:282-298)
+    const float theta = rr0 * 2.0f * HLSL_PI;
+    const float phi = hg_acosf(2.0f * rr1 - 1.0f);
+    const float sT = hg_sinf(theta), cT = hg_cosf(theta), sP = hg_sinf(phi), cP = hg_cosf(phi);
+    const f3 rv = mk(1.0f * sP * cT, 1.0f * sP * sT, 1.0f * cP);
+    const float rough2 = mt.prio_id_r2.z;
+    if (!(pr0 > mt.albedo.w)) {
+        att = xyz(mt.albedo);
+        const f3 diffuse = lambert(hit.n, rv);
+        const float metallic = mt.spec_metal.w;
+        const float thr = (metallic > 0.0f) ? schlick_adjusted(cur.ior, hm.ior, hit.n, ray.d, metallic, 1.0f)
+                                            : metallic;
+        const bool spec = pr1 < thr;
+        bt = spec ? 1u : 0u;
+        if (spec) {
+            ray.d = lerp(reflect(ray.d, hit.n), diffuse, rough2);
+            att = xyz(mt.spec_metal);
+        } else {
+            ray.d = diffuse;
+        }
+        ray.o = hit.pos + hit.n * 0.0001f;
+    } else {
+        bt = 2u;
+        att = mk(1, 1, 1);
+        bool tir = false;
+        ray.d = refract_tir(ray.d, hit.n, cur.ior, hm.ior, tir);
+        const f3 dd = tir ? lambert(hit.n, rv) : lambert(-hit.n, rv);
+        ray.d = lerp(ray.d, dd, rough2);
+        ray.o = hit.pos - hit.n * 0.0001f;
+    }
+    ray.d = normalize(ray.d);
+    return att;
+}
+
+// evaluate_material_hit :743-817
+__device__ f3 evaluate_hit(const HgKernelParams& kp, const Sampler& smp, MediumStack& ms, Ray& ray, const Hit& hit,
+                           const Mat& mt, Bounces& bounce) {
+    const Medium internal = medium_of(kp, hit.mat);
+    const int32_t prio = __float_as_int(mt.prio_id_r2.x);
+    Medium cur, hm;
+    bool trueHit = true;
+    if (prio >= 0) {
+        trueHit = ms.sp == 0 || prio <= mat_priority(kp, ms.get(ms.sp - 1));
+        if (hit.orient == 1.0f) {
+            cur = top_medium(kp, ms);
+            hm = internal;
+            medium_push(kp, ms, hit.mat);
+        } else {
+            cur = ms.sp == 0 ? internal : top_medium(kp, ms);
+            medium_pop(kp, ms, internal.id);
+            hm = top_medium(kp, ms);
+        }
+    } else {
+        if (hit.orient == 1.0f) {
+            cur = top_medium(kp, ms);
+            hm = internal;
+        } else {
+            cur = internal;
+            hm = top_medium(kp, ms);
+        }
+    }
+    f3 att;
+    if (trueHit) {
+        uint32_t bt = 0;
+        att = material_brdf(kp, smp, ray, hit, mt, cur, hm, bt);
+        bounce.bump(bt);
+        if (hit.orient > 0.0f && bt != 2u) medium_pop(kp, ms, internal.id);
+    } else {
+        ray.o = hit.pos - hit.n * 0.0001f;
+        att = mk(1, 1, 1);
+        bounce.transmission++;
+    }
+    if (cur.id != 0xFFFFFFFFu) {
+        att = mk(att.x * hg_expf(-cur.absorb.x * hit.t), att.y * hg_expf(-cur.absorb.y * hit.t),
+                 att.z * hg_expf(-cur.absorb.z * hit.t));
+    }
+    return att;
+}
+
+// trace_ray :876-950
+__device__ f3 trace_ray(const HgKernelParams& kp, Sampler& smp, MediumStack& ms, Ray ray, Counters& c,
+                        uint32_t* stack, uint32_t stride) {
+    f3 acc = mk(0, 0, 0), thr = mk(1, 1, 1);
+    float acc_rough = 0.0f;
+    Bounces bounce{0, 0, 0};
+    for (uint32_t it = 0; it <= kp.max_bounces; ++it) {
+        if (bounce.diffuse > kp.max_diff || bounce.glossy > kp.max_glossy || bounce.transmission > kp.max_trans)
+            break;
+        const Hit hit = intersect(kp, ray, c, stack, stride);
+        if (hit.t < kp.far_) {
+            c.hits++;
+            const Mat mt = load_mat(kp, hit.mat);
+            acc = acc + xyz(mt.emis_rough) * thr;
+            const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bounce);
+            thr = thr * att;
+            acc_rough += mt.emis_rough.w * thr.x;  // float3 -> float truncation (:911)
+            const float rr = smp.get1(ID_RR);
+            smp.offset += BOUNCE_INC;
+            const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
+            if (rr > contribution) break;
+            thr = thr * (1.0f / contribution);
+        } else {
+            acc = acc + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
+            break;
+        }
+    }
+    return acc;
+}
+
+// trace_ray_debug :952-982
+__device__ f3 trace_ray_debug(const HgKernelParams& kp, Sampler& smp, MediumStack& ms, Ray ray, Counters& c,
+                              uint32_t* stack, uint32_t stride) {
+    const uint32_t tri0 = c.tri, box0 = c.aabb;  // TriangleTests = AABBTests = 0
+    switch (kp.debug_mode) {
+        default:
+            return mk(0, 0, 0);
+        case 1: {
+            const Hit h = intersect(kp, ray, c, stack, stride);
+            if (h.t < kp.far_) return xyz(kp.materials[5 * h.mat]);
+            return sample_sky(kp, ray.d, kp.default_mip);
+        }
+        case 2: {
+            const Hit h = intersect(kp, ray, c, stack, stride);
+            if (h.t < kp.far_) return mk((h.n.x + 1.0f) / 2.0f, (h.n.y + 1.0f) / 2.0f, (h.n.z + 1.0f) / 2.0f);
+            return sample_sky(kp, ray.d, kp.default_mip);
+        }
+        case 3:
+        case 4:
+        case 5: {
+            trace_ray(kp, smp, ms, ray, c, stack, stride);
+            const uint32_t tt = c.tri - tri0, bb = c.aabb - box0;
+            if (kp.debug_mode == 3) {
+                if (tt > kp.tri_range) return mk(1, 1, 1);
+                return mk(float(tt) / float(kp.tri_range), 0, 0);
+            }
+            if (kp.debug_mode == 4) {
+                if (bb > kp.box_range) return mk(1, 1, 1);
+                return mk(float(bb) / float(kp.box_range), 0, 0);
+            }
+            if (tt > kp.tri_range || bb > kp.box_range) return mk(1, 1, 1);
+            return mk(float(tt) / float(kp.tri_range), 0, float(bb) / float(kp.box_range));
+        }
+    }
+}
+
+// inverted_blackman_harris_cdf_approximation (HalogenRandom.hlsl:319-330)
+__device__ __forceinline__ float inv_blackman_harris(float x) {
+    const float a = (x * 1.99221575606f) - 0.99610787803f;
+    return (0.5f * hg_logf((1.0f + a) / (1.0f - a))) / 6.24f;
+}
+
+// get_ray :996-1013 (+ get_ray_jitter :984-994, get_random_point_circle HalogenRandom.hlsl:303-308)
+__device__ Ray camera_ray(const HgKernelParams& kp, const Sampler& smp, float ndcx, float ndcy) {
+    float fd0, fd1, j0, j1;
+    smp.get2(ID_FOCAL, fd0, fd1);
+    const float th = (fd0 * 360.0f) * HG_DEG2RAD;
+    const f3 ap = mk(hg_cosf(th) * kp.focal_disc_radius * fd1, hg_sinf(th) * kp.focal_disc_radius * fd1, 0.0f);
+    f3 screen = mk(ndcx * kp.vw, ndcy * kp.vh, 1.0f * kp.near_);
+    smp.get2(ID_JITTER, j0, j1);
+    const float jx = (inv_blackman_harris(j0) - 0.5f) * 2.0f * kp.filter_radius * kp.psx;
+    const float jy = (inv_blackman_harris(j1) - 0.5f) * 2.0f * kp.filter_radius * kp.psy;
+    screen = screen + mk(jx, jy, 0.0f);
+    const f3 pf = normalize(screen) * kp.focal_dist;
+    const f3 csd = normalize(pf - ap);
+    Ray r;
+    r.o = xform(kp.cam, ap, 1.0f);
+    r.d = normalize(xform(kp.cam, csd, 0.0f));
+    return r;
+}
+
+// wave64 sum (all 64 lanes active at the call site)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace
+
+template <bool kCounters>
+__global__ __launch_bounds__(256) void hg_trace_kernel(const HgKernelParams kp) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t lane = threadIdx.x & 63u;
+    const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    const int gtile = kp.rank + local_tile * kp.n_ranks;
+    const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+    const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+    const bool active = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu;
+    Counters c{0, 0, 0, 0, 0, 0};
+    uint32_t paths = 0;
+    if (active) {
+        uint32_t* stack = lds_stack + threadIdx.x;
+        const uint32_t stride = blockDim.x;
+        const size_t slot = size_t(local_tile) * 64 + lane;
+        float4 acc = kp.acc[slot];
+        // HalogenCompute :1023-1033
+        const float ndcx = (float(px) / kp.W) * 2.0f - 1.0f;
+        const float ndcy = (float(py) / kp.H) * 2.0f - 1.0f;
+        const uint32_t pixel_id = pcg_hash(px + py * kp.Wu);
+        for (int f = 0; f < kp.n_frames; ++f) {
+            const int32_t fc = kp.accumulate ? kp.first_frame + f : 1;
+            Sampler smp{uint32_t(fc), pixel_id, 0u};
+            MediumStack ms{0ull, 0};
+            f3 color = mk(0, 0, 0);
+            for (uint32_t s = 0; s < kp.spp; ++s) {
+                const Ray r = camera_ray(kp, smp, ndcx, ndcy);
+                paths++;
+                if (kp.debug_mode < 1) color = color + trace_ray(kp, smp, ms, r, c, stack, stride);
+                else color = color + trace_ray_debug(kp, smp, ms, r, c, stack, stride);
+            }
+            const float sppf = float(kp.spp);
+            color = mk(color.x / sppf, color.y / sppf, color.z / sppf);
+            if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
+                const float w = 1.0f / float(fc);
+                const float k = 1.0f - w;
+                acc.x = acc.x * k + color.x * w;
+                acc.y = acc.y * k + color.y * w;
+                acc.z = acc.z * k + color.z * w;
+                acc.w = acc.w * k + 1.0f * w;
+            } else {
+                acc = make_float4(color.x, color.y, color.z, 1.0f);
+            }
+        }
+        kp.acc[slot] = acc;
+    }
+    if (kCounters) {
+        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.meshes, c.spheres, c.hits};
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const uint32_t s = wave_sum(v[k]);
+            if (lane == 0 && s) atomicAdd(kp.counters + k, (unsigned long long)s);
+        }
+    }
+}
+
+// Launcher used by the runtime (hg_runtime.hip)
+hipError_t hg_launch_trace(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
+    const int tiles_per_block = block / 64;
+    const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
+    if (grid == 0) return hipSuccess;
+    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    if (counters)
+        hipLaunchKernelGGL(hg_trace_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
+    else
+        hipLaunchKernelGGL(hg_trace_kernel<false>, dim3(grid), dim3(block), lds, stream, kp);
+    return hipGetLastError();
+}

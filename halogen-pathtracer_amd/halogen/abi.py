@@ -1,0 +1,257 @@
+"""ctypes mirror of include/halogen_abi.h and a thin, error-checked wrapper around libhalogen_hip.so.
+
+The structs below are byte-identical to the reference's C# blittable structs
+(Assets/Scripts/Render Features/HalogenRenderPass.cs:10-76); test_abi.py checks every size and offset
+against the header.  There is no fallback: if the shared library is missing, importing `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libhalogen_hip.so"
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Vec4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class Mat4(C.Structure):
+    """UnityEngine.Matrix4x4 field order (m00, m10, m20, m30, m01, ...): column-major."""
+
+    _fields_ = [("m", C.c_float * 16)]
+
+
+class HalogenSphere(C.Structure):  # RP:10-19, 44 B
+    _fields_ = [("center", Vec3), ("radius", C.c_float), ("materialIndex", C.c_uint32),
+                ("boundingCornerA", Vec3), ("boundingCornerB", Vec3)]
+
+
+class HalogenMeshData(C.Structure):  # RP:21-34, 164 B
+    _fields_ = [("triangleBufferOffset", C.c_uint32), ("accelerationBufferOffset", C.c_uint32),
+                ("boundingCornerA", Vec3), ("boundingCornerB", Vec3), ("materialIndex", C.c_uint32),
+                ("worldToLocal", Mat4), ("localToWorld", Mat4)]
+
+
+class PackedRayMedium(C.Structure):  # RP:36-42, 24 B
+    _fields_ = [("indexOfRefraction", C.c_float), ("absorption", Vec3), ("priority", C.c_int32),
+                ("materialID", C.c_uint32)]
+
+
+class PackedHalogenMaterial(C.Structure):  # RP:44-55, 84 B
+    _fields_ = [("materialID", C.c_uint32), ("albedo", Vec4), ("specularAlbedo", Vec4), ("metallic", C.c_float),
+                ("roughness", C.c_float), ("emissive", Vec4), ("rayMedium", PackedRayMedium)]
+
+
+class HalogenTriangle(C.Structure):  # RP:57-66, 72 B
+    _fields_ = [("pointA", Vec3), ("pointB", Vec3), ("pointC", Vec3), ("normalA", Vec3), ("normalB", Vec3),
+                ("normalC", Vec3)]
+
+
+class BVHEntry(C.Structure):  # RP:68-76, 32 B
+    _fields_ = [("indexA", C.c_uint32), ("triangleCount", C.c_uint32), ("boundingCornerA", Vec3),
+                ("boundingCornerB", Vec3)]
+
+
+class HgParams(C.Structure):  # every uniform of HalgoenCompute.compute:26-68,185
+    _fields_ = [
+        ("camLocalToWorld", Mat4), ("screenParameters", Vec4), ("viewParameters", Vec4),
+        ("cameraParameters", Vec4), ("frameCount", C.c_int32), ("samplesPerPixel", C.c_uint32),
+        ("maxBounces", C.c_uint32), ("maxDiffuseBounces", C.c_uint32), ("maxGlossyBounces", C.c_uint32),
+        ("maxTransmissionBounces", C.c_uint32), ("halogenDebugMode", C.c_uint32),
+        ("triangleDebugDisplayRange", C.c_uint32), ("boxDebugDisplayRange", C.c_uint32),
+        ("defaultHDRIMipLevel", C.c_int32), ("focalPlaneDistance", C.c_float), ("focalConeAngle", C.c_float),
+        ("filterRadius", C.c_float), ("useEnvironmentCubemap", C.c_int32), ("bufferCounts", Vec4),
+    ]
+
+
+class HgCounters(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
+                ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+HG_OK = 0
+HG_KERNEL_MEGA, HG_KERNEL_PERSISTENT = 0, 1
+HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS = 1, 2, 3
+
+# every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
+EXPORTS = [
+    "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
+    "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
+    "hg_readback", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
+    "hg_set_option", "hg_build_blas", "hg_unity_bounds", "hg_pack_triangles",
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libhalogen_hip.so (built in-tree by `make -C halogen-pathtracer_amd`).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"{LIB_PATH} not built: run `make -C halogen-pathtracer_amd` (no CPU fallback exists)")
+    L = C.CDLL(str(LIB_PATH))
+    P = C.c_void_p
+    i32, i64, sz, f32p = C.c_int32, C.c_int64, C.c_size_t, C.POINTER(C.c_float)
+    sig = {
+        "hg_abi_version": (C.c_int, []),
+        "hg_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+        "hg_destroy": (None, [P]),
+        "hg_last_error": (C.c_char_p, [P]),
+        "hg_upload_scene": (C.c_int, [P, P, i32, P, i32, P, i32, P, i32, P, i32]),
+        "hg_upload_cubemap": (C.c_int, [P, i32, i32, P, sz]),
+        "hg_set_params": (C.c_int, [P, C.POINTER(HgParams)]),
+        "hg_resize": (C.c_int, [P, i32, i32]),
+        "hg_set_tiling": (C.c_int, [P, i32, i32]),
+        "hg_clear_accumulation": (C.c_int, [P]),
+        "hg_render": (C.c_int, [P, i32, i32]),
+        "hg_synchronize": (C.c_int, [P]),
+        "hg_readback": (C.c_int, [P, f32p, sz]),
+        "hg_copy_tiles_device": (C.c_int, [P, P, sz]),
+        "hg_local_tile_count": (i32, [P]),
+        "hg_get_counters": (C.c_int, [P, C.POINTER(HgCounters)]),
+        "hg_reset_counters": (C.c_int, [P]),
+        "hg_set_option": (C.c_int, [P, i32, i32]),
+        "hg_build_blas": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64]),
+        "hg_unity_bounds": (None, [f32p, f32p, i32, f32p, f32p]),
+        "hg_pack_triangles": (C.c_int, [P, P, i32, P, i32, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class HalogenError(RuntimeError):
+    pass
+
+
+def _ptr(a) -> C.c_void_p:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return C.c_void_p(a.ctypes.data)
+    return C.cast(a, C.c_void_p)
+
+
+def as_struct_array(struct_type, n: int):
+    return (struct_type * max(n, 0))()
+
+
+class Context:
+    """One HIP device + stream (hg_ctx).  Not thread-safe; one per GPU."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.hg_create(int(device), C.byref(h))
+        if rc != HG_OK:
+            raise HalogenError(f"hg_create(device={device}) failed with {rc} (no usable HIP device?)")
+        self._h = h
+        self.device = device
+
+    def _check(self, rc: int, what: str):
+        if rc != HG_OK:
+            msg = lib().hg_last_error(self._h)
+            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().hg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # --- API -----------------------------------------------------------------------------------------
+    def upload_scene(self, packed) -> None:
+        """packed: halogen.scene.PackedScene (ctypes arrays of the reference structs)."""
+        self._check(lib().hg_upload_scene(
+            self._h, _ptr(packed.spheres), len(packed.spheres), _ptr(packed.meshes), len(packed.meshes),
+            _ptr(packed.materials), len(packed.materials), _ptr(packed.triangles), len(packed.triangles),
+            _ptr(packed.blas), len(packed.blas)), "hg_upload_scene")
+
+    def upload_cubemap(self, face_size: int, n_mips: int, texels: np.ndarray) -> None:
+        t = np.ascontiguousarray(texels, dtype=np.float32)
+        self._check(lib().hg_upload_cubemap(self._h, face_size, n_mips, _ptr(t), t.size), "hg_upload_cubemap")
+
+    def set_params(self, p: HgParams) -> None:
+        self._check(lib().hg_set_params(self._h, C.byref(p)), "hg_set_params")
+
+    def resize(self, w: int, h: int) -> None:
+        self._check(lib().hg_resize(self._h, w, h), "hg_resize")
+
+    def set_tiling(self, rank: int, n_ranks: int) -> None:
+        self._check(lib().hg_set_tiling(self._h, rank, n_ranks), "hg_set_tiling")
+
+    def clear_accumulation(self) -> None:
+        self._check(lib().hg_clear_accumulation(self._h), "hg_clear_accumulation")
+
+    def render(self, n_frames: int, accumulate: bool = True) -> None:
+        self._check(lib().hg_render(self._h, int(n_frames), 1 if accumulate else 0), "hg_render")
+
+    def synchronize(self) -> None:
+        self._check(lib().hg_synchronize(self._h), "hg_synchronize")
+
+    def readback(self, w: int, h: int, out: np.ndarray | None = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros((h, w, 4), dtype=np.float32)
+        self._check(lib().hg_readback(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size), "hg_readback")
+        return out
+
+    def local_tile_count(self) -> int:
+        return int(lib().hg_local_tile_count(self._h))
+
+    def copy_tiles_device(self, dst_ptr: int, n_bytes: int) -> None:
+        self._check(lib().hg_copy_tiles_device(self._h, C.c_void_p(dst_ptr), n_bytes), "hg_copy_tiles_device")
+
+    def counters(self) -> dict:
+        c = HgCounters()
+        self._check(lib().hg_get_counters(self._h, C.byref(c)), "hg_get_counters")
+        return c.as_dict()
+
+    def reset_counters(self) -> None:
+        self._check(lib().hg_reset_counters(self._h), "hg_reset_counters")
+
+    def set_option(self, option: int, value: int) -> None:
+        self._check(lib().hg_set_option(self._h, option, value), "hg_set_option")
+
+
+def gpu_available() -> bool:
+    """True when a HIP device is visible (without initialising torch)."""
+    if os.environ.get("HIP_VISIBLE_DEVICES") == "":
+        return False
+    try:
+        L = lib()
+    except RuntimeError:
+        return False
+    h = C.c_void_p()
+    if L.hg_create(0, C.byref(h)) != HG_OK:
+        return False
+    L.hg_destroy(h)
+    return True

@@ -1,0 +1,49 @@
+"""Multi-GPU framebuffer tiling (not in the reference, which is single-GPU).
+
+Pixels are independent: a pixel's value depends only on the scene, the uniforms, its GLOBAL index and
+FrameCount (HalgoenCompute.compute:1033).  So the image's 8x8 tiles are dealt round-robin to ranks
+(tile t -> rank t % N, which balances the centre-heavy dragon), every rank traces and accumulates all
+frames of its own tiles, and the only collective is one gather of the packed accumulated tiles at the end.
+One process per GPU; torch.distributed is the transport (backend "nccl" = RCCL over xGMI on ROCm, "gloo" in
+CPU tests).  The gathered image is bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
+tests/test_distributed_cpu.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+TILE = 8
+
+
+def tiles_xy(width: int, height: int) -> tuple[int, int]:
+    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+
+
+def local_tile_count(total_tiles: int, rank: int, n_ranks: int) -> int:
+    return max(0, (total_tiles - rank + n_ranks - 1) // n_ranks)
+
+
+def gather_tiles(local: torch.Tensor, rank: int, n_ranks: int, width: int, height: int) -> torch.Tensor | None:
+    """local: (n_local_tiles, 64, 4) float32 tiles of this rank (hg_copy_tiles_device layout).
+    Returns the (height, width, 4) image on rank 0 (None elsewhere).  One all_gather_into_tensor of
+    max-local-tiles x 1 KiB per rank (ranks hold ceil/floor shares, padded to the max)."""
+    tx, ty = tiles_xy(width, height)
+    total = tx * ty
+    max_local = local_tile_count(total, 0, n_ranks)
+    buf = torch.zeros((max_local, 64, 4), dtype=torch.float32, device=local.device)
+    buf[: local.shape[0]] = local
+    out = torch.empty((n_ranks * max_local, 64, 4), dtype=torch.float32, device=local.device)
+    dist.all_gather_into_tensor(out, buf)
+    if rank != 0:
+        return None
+    return untile(out.view(n_ranks, max_local, 64, 4), n_ranks, width, height)
+
+
+def untile(per_rank: torch.Tensor, n_ranks: int, width: int, height: int) -> torch.Tensor:
+    """(n_ranks, max_local, 64, 4) -> (height, width, 4): global tile g lives at rank g % N, slot g // N."""
+    tx, ty = tiles_xy(width, height)
+    g = torch.arange(tx * ty, device=per_rank.device)
+    tiles = per_rank[g % n_ranks, g // n_ranks]  # (total, 64, 4) in global tile order
+    img = tiles.view(ty, tx, TILE, TILE, 4).permute(0, 2, 1, 3, 4).reshape(ty * TILE, tx * TILE, 4)
+    return img[:height, :width]

@@ -1,0 +1,210 @@
+"""HalogenSettings + HalogenRenderPass — the host-side API surface of the reference, over the C-ABI.
+
+Mirrors Assets/Scripts/Render Features/HalogenRenderFeature.cs:25-67 (settings) and
+Assets/Scripts/Render Features/HalogenRenderPass.cs (RP) — the constructor's clamping (RP:154-233),
+OnCameraSetup (RP:237-260), ClearAccumulation (RP:262-268), Execute (RP:270-357), DispatchHalogenTrace's
+uniform derivation (RP:359-401), Dispose (RP:410-423) and getFrameCount (RP:548).  Unity's
+ComputeShader/ComputeBuffer/RTHandle/Blit calls are replaced by the hg_* entry points (abi.Context).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .unity import Transform, to_unity_floats
+
+f32 = np.float32
+
+DEBUG_MODES = {"None": 0, "Albedo": 1, "Normal": 2, "RayTriangleTests": 3, "RayBoxTests": 4, "Combined": 5}
+
+
+@dataclass
+class HalogenSettings:
+    """Defaults are the values of Assets/URP-HighFidelity-Renderer.asset:51-77."""
+
+    ShowInSceneView: bool = True
+    Accumulate: bool = True
+    SamplesPerPixel: int = 1
+    MaxAccumulatedFrames: int = 16
+    UnlimitedSampling: bool = True
+    MaxBounces: int = 12
+    DiffuseBounces: int = 4
+    GlossyBounces: int = 4
+    TransmissionBounces: int = 12
+    FilterRadius: float = 1.0
+    NearPlaneDistance: float = 0.1
+    FarPlaneDistance: float = 5000.0
+    FocalPlaneDistance: float = 8.18
+    ApertureAngle: float = 0.0
+    useHDRISky: bool = True
+    environmentCubemap: object = None  # halogen.envmap.Cubemap or None
+    EnvironmentMipLevel: int = 1
+    FirstInteractionOnly: bool = True
+    DebugMode: str = "None"
+    TriangleDebugDisplayRange: int = 100
+    BoxDebugDisplayRange: int = 153
+
+
+@dataclass
+class Camera:
+    """The Unity camera the pass renders for: transform, vertical FOV (degrees) and pixel size."""
+
+    transform: Transform = field(default_factory=Transform)
+    fieldOfView: float = 60.0
+    pixelWidth: int = 256
+    pixelHeight: int = 256
+
+    @property
+    def aspect(self) -> float:
+        return float(f32(self.pixelWidth) / f32(self.pixelHeight))
+
+    def pose(self):
+        return (self.transform.position_local, self.transform.rotation_local)
+
+
+def make_params(settings_clamped: dict, camera: Camera, frame_count: int, n_spheres: int, n_meshes: int,
+                use_cubemap: bool) -> abi.HgParams:
+    """DispatchHalogenTrace, RP:359-401: every uniform, derived in float32 the way the C# code does."""
+    s = settings_clamped
+    p = abi.HgParams()
+    n_clip = f32(s["NearPlaneDistance"])
+    deg2rad = f32(math.pi / 180.0)  # Mathf.Deg2Rad
+    half = f32(deg2rad * f32(camera.fieldOfView)) * f32(0.5)
+    h = f32(math.tan(float(half))) * n_clip  # Mathf.Tan = (float)Math.Tan
+    w = f32(camera.aspect) * h
+    p.camLocalToWorld.m[:] = to_unity_floats(camera.transform.local_to_world)
+    p.screenParameters = abi.Vec4(camera.pixelWidth, camera.pixelHeight, 0.0, 0.0)
+    p.viewParameters = abi.Vec4(float(w), float(h), float(n_clip), float(f32(s["FarPlaneDistance"])))
+    pos = camera.transform.position
+    p.cameraParameters = abi.Vec4(float(pos[0]), float(pos[1]), float(pos[2]), 0.0)
+    p.frameCount = frame_count if s["Accumulate"] else 1
+    p.samplesPerPixel = s["SamplesPerPixel"]
+    p.maxBounces = s["MaxBounces"]
+    p.maxDiffuseBounces = s["MaxDiffuseBounces"]
+    p.maxGlossyBounces = s["MaxGlossyBounces"]
+    p.maxTransmissionBounces = s["MaxTransmissionBounces"]
+    p.halogenDebugMode = s["HalogenDebugMode"]
+    p.triangleDebugDisplayRange = s["TriangleDebugDisplayRange"]
+    p.boxDebugDisplayRange = s["BoxDebugDisplayRange"]
+    p.defaultHDRIMipLevel = s["EnvironmentMipLevel"]
+    p.focalPlaneDistance = s["FocalPlaneDistance"]
+    p.focalConeAngle = s["ApertureAngle"]
+    p.filterRadius = s["FilterRadius"]
+    p.useEnvironmentCubemap = 1 if use_cubemap else 0
+    p.bufferCounts = abi.Vec4(n_spheres, n_meshes, 0.0, 0.0)
+    return p
+
+
+def clamp_settings(st: HalogenSettings) -> dict:
+    """The constructor's clamping and debug-mode mapping, RP:169-231."""
+    eps = 1.401298464324817e-45  # Mathf.Epsilon (smallest denormal float)
+    d = {}
+    d["SamplesPerPixel"] = max(1, int(st.SamplesPerPixel))
+    d["MaxBounces"] = max(0, int(st.MaxBounces))
+    d["MaxDiffuseBounces"] = max(0, int(st.DiffuseBounces))
+    d["MaxGlossyBounces"] = max(0, int(st.GlossyBounces))
+    d["MaxTransmissionBounces"] = max(0, int(st.TransmissionBounces))
+    d["FilterRadius"] = max(0.0, float(st.FilterRadius))
+    d["FocalPlaneDistance"] = max(eps, float(st.FocalPlaneDistance))
+    d["NearPlaneDistance"] = max(eps, float(st.NearPlaneDistance))
+    d["FarPlaneDistance"] = max(float(f32(d["NearPlaneDistance"]) + f32(eps)), float(st.FarPlaneDistance))
+    d["ApertureAngle"] = min(max(float(st.ApertureAngle), 0.0), 89.9)
+    d["EnvironmentMipLevel"] = min(max(int(st.EnvironmentMipLevel), 0), 2)
+    d["Accumulate"] = bool(st.Accumulate)
+    d["MaxAccumulatedFrames"] = max(int(st.MaxAccumulatedFrames), 1)
+    d["UnlimitedSampling"] = bool(st.UnlimitedSampling)
+    use = bool(st.useHDRISky) and st.environmentCubemap is not None
+    d["UseEnvironmentCubemap"] = use
+    mode = DEBUG_MODES.get(st.DebugMode, 0) if isinstance(st.DebugMode, str) else int(st.DebugMode)
+    d["HalogenDebugMode"] = mode
+    if mode != 0 and st.FirstInteractionOnly:
+        d["MaxBounces"] = 0
+    d["TriangleDebugDisplayRange"] = max(int(st.TriangleDebugDisplayRange), 1)
+    d["BoxDebugDisplayRange"] = max(int(st.BoxDebugDisplayRange), 1)
+    return d
+
+
+class HalogenRenderPass:
+    """Progressive path tracing of a `halogen.scene.Scene` on one GPU (or one rank's tiles)."""
+
+    def __init__(self, settings: HalogenSettings, device: int = 0, context: abi.Context | None = None):
+        self.settings = settings
+        self.s = clamp_settings(settings)
+        self.ctx = context if context is not None else abi.Context(device)
+        self.FrameCount = 1
+        self.AccumulationBufferDirty = True
+        self.ObjectBuffersDirty = True
+        self._prior_pose = None
+        self._prior_resolution = None
+        self._scene_counts = (0, 0)
+        self._cubemap_uploaded = False
+        self.rank, self.n_ranks = 0, 1
+
+    # ---- RP:237-268 ----------------------------------------------------------------------------
+    def OnCameraSetup(self, width: int, height: int):
+        res = (int(width), int(height))
+        if res != self._prior_resolution:
+            self.ctx.resize(*res)
+            self.ClearAccumulation()
+        self._prior_resolution = res
+
+    def ClearAccumulation(self):
+        self.FrameCount = 1
+        self.AccumulationBufferDirty = True
+        self.ObjectBuffersDirty = True
+
+    def set_tiling(self, rank: int, n_ranks: int):
+        """Multi-GPU: render only the 8x8 tiles t with t % n_ranks == rank (not in the reference)."""
+        self.rank, self.n_ranks = rank, n_ranks
+        self.ctx.set_tiling(rank, n_ranks)
+        self.ClearAccumulation()
+
+    def UpdateObjectBuffers(self, scene):
+        packed = scene.pack() if hasattr(scene, "pack") else scene
+        self.ctx.upload_scene(packed)
+        self._scene_counts = (len(packed.spheres), len(packed.meshes))
+        cube = self.settings.environmentCubemap
+        if self.s["UseEnvironmentCubemap"] and not self._cubemap_uploaded:
+            self.ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+            self._cubemap_uploaded = True
+        return packed
+
+    # ---- RP:270-357 ----------------------------------------------------------------------------
+    def Execute(self, scene, camera: Camera, n_frames: int = 1):
+        """One Execute per frame in the reference; n_frames > 1 runs that many frames in ONE dispatch with the
+        identical per-frame semantics (FrameCount advancing, same blend) as long as nothing changes between."""
+        self.OnCameraSetup(camera.pixelWidth, camera.pixelHeight)
+        pose = camera.pose()
+        if self._prior_pose is not None and pose != self._prior_pose:
+            self.ClearAccumulation()
+        if self.FrameCount > 1 and not self.s["Accumulate"]:
+            self.ClearAccumulation()
+        self._prior_pose = pose
+        if self.ObjectBuffersDirty:
+            self.UpdateObjectBuffers(scene)
+            self.ObjectBuffersDirty = False
+        if not self.s["UnlimitedSampling"] and self.FrameCount > self.s["MaxAccumulatedFrames"]:
+            return  # rendering done: the reference only re-blits the finished image
+        if not self.s["UnlimitedSampling"]:
+            n_frames = min(n_frames, self.s["MaxAccumulatedFrames"] - self.FrameCount + 1)
+        p = make_params(self.s, camera, self.FrameCount, *self._scene_counts, self.s["UseEnvironmentCubemap"])
+        self.ctx.set_params(p)
+        if self.AccumulationBufferDirty:
+            self.ctx.clear_accumulation()
+            self.AccumulationBufferDirty = False
+        self.ctx.render(n_frames, accumulate=self.s["Accumulate"])
+        if self.s["Accumulate"]:
+            self.FrameCount += n_frames
+
+    def read_image(self) -> np.ndarray:
+        w, h = self._prior_resolution
+        return self.ctx.readback(w, h)
+
+    def getFrameCount(self) -> int:
+        return self.FrameCount
+
+    def Dispose(self):
+        self.ctx.close()

@@ -1,0 +1,242 @@
+/*
+ * halogen_abi.h — the drop-in C-ABI boundary of the Halogen path-tracing hot path on MI355X (gfx950).
+ *
+ * What it replaces (reference: /root/reference, Unity 2022.3 + URP 14):
+ *   The ComputeShader / ComputeBuffer / RTHandle calls inside
+ *   `Assets/Scripts/Render Features/HalogenRenderPass.cs` ("RP" below):
+ *     - buffer (re)allocation            RP:498-502, RP:539-546  -> hg_upload_scene (copies, owns device memory)
+ *     - buffer uploads (SetBufferData)   RP:504-508              -> hg_upload_scene
+ *     - cubemap binding                  RP:397-398              -> hg_upload_cubemap
+ *     - uniform binding                  RP:360-401              -> hg_set_params
+ *     - RTHandle allocation on resize    RP:237-260              -> hg_resize
+ *     - ClearAccumulation                RP:262-268, RP:333-338  -> hg_clear_accumulation
+ *     - DispatchCompute + accumulation   RP:324-347, RP:406      -> hg_render (trace + fused accumulate)
+ *       blit (AccumulationShader.shader:27-34)
+ *     - Dispose / Release                RP:410-423              -> hg_destroy
+ *   plus what the reference never had: readback, counters, error text, multi-GPU tiling.
+ *
+ * The host structs below are byte-identical to the reference's C# blittable structs
+ * (RP:10-76, strides from Marshal.SizeOf at RP:163-167): a C# caller passes its List<T>.ToArray()
+ * unchanged through P/Invoke.  Device-side layouts are private to the library
+ * (SoA / child-pair records, repacked inside hg_upload_scene).
+ *
+ * Conventions:
+ *   - every int-returning function returns HG_OK (0) or a negative HG_E_* code; hg_last_error() has text.
+ *   - host arrays are copied during the call (SetBufferData semantics); counts of 0 are legal.
+ *   - one context = one device + one HIP stream; a context is NOT thread-safe; one context per GPU may be
+ *     driven from separate host threads.  hg_render is asynchronous; hg_readback / hg_synchronize block.
+ *   - no torch / HIP types appear in any signature.
+ */
+#ifndef HALOGEN_ABI_H
+#define HALOGEN_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_ABI_VERSION 1
+
+/* ----------------------------------------------------------------------------------------------
+ * Reference host structs (byte-identical to the C# [Sequential] structs)
+ * -------------------------------------------------------------------------------------------- */
+typedef struct hg_vec3 { float x, y, z; } hg_vec3;
+typedef struct hg_vec4 { float x, y, z, w; } hg_vec4;
+
+/* UnityEngine.Matrix4x4: fields m00,m10,m20,m30,m01,... i.e. column-major; element (r,c) = m[c*4+r].
+ * HLSL mul(M, v) in the reference = sum_c M(r,c) * v_c. */
+typedef struct hg_mat4 { float m[16]; } hg_mat4;
+
+/* HalogenSphere, RP:10-19 (44 B) */
+typedef struct HalogenSphere {
+    hg_vec3 center;
+    float radius;
+    uint32_t materialIndex;
+    hg_vec3 boundingCornerA;
+    hg_vec3 boundingCornerB;
+} HalogenSphere;
+
+/* HalogenMeshData, RP:21-34 (164 B) */
+typedef struct HalogenMeshData {
+    uint32_t triangleBufferOffset;
+    uint32_t accelerationBufferOffset;
+    hg_vec3 boundingCornerA;
+    hg_vec3 boundingCornerB;
+    uint32_t materialIndex;
+    hg_mat4 worldToLocal;
+    hg_mat4 localToWorld;
+} HalogenMeshData;
+
+/* PackedRayMedium, RP:36-42 (24 B) */
+typedef struct PackedRayMedium {
+    float indexOfRefraction;
+    hg_vec3 absorption;
+    int32_t priority;
+    uint32_t materialID;
+} PackedRayMedium;
+
+/* PackedHalogenMaterial, RP:44-55 (84 B) */
+typedef struct PackedHalogenMaterial {
+    uint32_t materialID;
+    hg_vec4 albedo;
+    hg_vec4 specularAlbedo;
+    float metallic;
+    float roughness;
+    hg_vec4 emissive;
+    PackedRayMedium rayMedium;
+} PackedHalogenMaterial;
+
+/* HalogenTriangle, RP:57-66 (72 B) */
+typedef struct HalogenTriangle {
+    hg_vec3 pointA, pointB, pointC;
+    hg_vec3 normalA, normalB, normalC;
+} HalogenTriangle;
+
+/* BVHEntry, RP:68-76 (32 B).  triangleCount > 0: leaf, indexA = first triangle (mesh-relative);
+ * triangleCount == 0: inner node, children at indexA and indexA+1 (mesh-relative node indices). */
+typedef struct BVHEntry {
+    uint32_t indexA;
+    uint32_t triangleCount;
+    hg_vec3 boundingCornerA;
+    hg_vec3 boundingCornerB;
+} BVHEntry;
+
+/* ----------------------------------------------------------------------------------------------
+ * Uniform block: every shader uniform of HalgoenCompute.compute:26-68,185, as set by
+ * DispatchHalogenTrace (RP:359-401).  Field order is ours; meanings are the reference's.
+ * -------------------------------------------------------------------------------------------- */
+typedef struct hg_params {
+    hg_mat4 camLocalToWorld;        /* CamLocalToWorldMatrix = camera.transform.localToWorldMatrix (RP:366) */
+    hg_vec4 screenParameters;       /* (pixelWidth, pixelHeight, 0, 0) (RP:367) */
+    hg_vec4 viewParameters;         /* (w, h, near, far) with h = tan(fov/2)*near, w = aspect*h (RP:361-368) */
+    hg_vec4 cameraParameters;       /* camera position (RP:369) — dead in the kernel, kept for fidelity */
+    int32_t frameCount;             /* FrameCount of the FIRST frame hg_render traces (RP:378) */
+    uint32_t samplesPerPixel;       /* RP:382 */
+    uint32_t maxBounces;            /* RP:383 */
+    uint32_t maxDiffuseBounces;     /* RP:384 */
+    uint32_t maxGlossyBounces;      /* RP:385 */
+    uint32_t maxTransmissionBounces;/* RP:386 */
+    uint32_t halogenDebugMode;      /* 0 none, 1 albedo, 2 normal, 3 tri tests, 4 box tests, 5 combined (RP:389) */
+    uint32_t triangleDebugDisplayRange; /* RP:390 */
+    uint32_t boxDebugDisplayRange;  /* RP:391 */
+    int32_t defaultHDRIMipLevel;    /* RP:379 */
+    float focalPlaneDistance;       /* RP:393 */
+    float focalConeAngle;           /* aperture angle in degrees (RP:394) */
+    float filterRadius;             /* pixels (RP:395) */
+    int32_t useEnvironmentCubemap;  /* RP:398 */
+    hg_vec4 bufferCounts;           /* (spheres, meshes, 0, 0) (RP:381) */
+} hg_params;
+
+/* Work / traffic counters, summed over every traced path since the last hg_reset_counters.
+ * tri_tests / aabb_tests are the reference's TriangleTests / AABBTests (HalgoenCompute.compute:412,428). */
+typedef struct hg_counters {
+    uint64_t paths;        /* pixel-samples traced (W*H*SPP per frame) */
+    uint64_t rays;         /* get_ray_intersection calls (bounce iterations reaching :895) */
+    uint64_t tri_tests;    /* triangle_intersection_doublesided calls */
+    uint64_t aabb_tests;   /* ray_AABB_test calls inside BLAS traversal (2 per inner node visit) */
+    uint64_t mesh_visits;  /* rays x meshes (world->local transforms) */
+    uint64_t sphere_tests; /* rays x spheres (sphere AABB prefilters) */
+    uint64_t hits;         /* accepted hits (hit.rayT < far) */
+    double kernel_ms;      /* summed device time of the trace kernel (HIP events on the context stream) */
+    uint64_t launches;     /* trace kernel launches */
+} hg_counters;
+
+typedef struct hg_ctx hg_ctx;
+
+enum {
+    HG_OK = 0,
+    HG_E_INVALID = -1,   /* bad argument / state */
+    HG_E_HIP = -2,       /* HIP runtime error (text from hipGetErrorString) */
+    HG_E_NOMEM = -3,
+    HG_E_NOSCENE = -4,
+    HG_E_NOTARGET = -5,  /* hg_resize not called */
+    HG_E_UNSUPPORTED = -6
+};
+
+/* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v). */
+enum { HG_KERNEL_MEGA = 0, HG_KERNEL_PERSISTENT = 1 };
+enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3 };
+
+int hg_abi_version(void);
+
+/* Create a context on HIP device `device` (ordinal as seen by the process). */
+int hg_create(int device, hg_ctx** out);
+void hg_destroy(hg_ctx* ctx);
+const char* hg_last_error(const hg_ctx* ctx);
+
+/* Upload the scene buffers (UpdateObjectBuffers, RP:448-509).  Validates every cross-reference
+ * (offsets, child indices, material indices) before anything reaches the GPU. */
+int hg_upload_scene(hg_ctx* ctx,
+                    const HalogenSphere* spheres, int32_t n_spheres,
+                    const HalogenMeshData* meshes, int32_t n_meshes,
+                    const PackedHalogenMaterial* materials, int32_t n_materials,
+                    const HalogenTriangle* triangles, int32_t n_triangles,
+                    const BVHEntry* blas, int32_t n_nodes);
+
+/* Environment cubemap (EnvironmentCubemap, HalgoenCompute.compute:48): RGBA32F texels, layout
+ * [mip][face][y][x][4], faces +X,-X,+Y,-Y,+Z,-Z, mip m is max(1, face_size >> m) square.
+ * Sampling is the manual bilinear defined in DESIGN.md §cubemap (shared with the oracle). */
+int hg_upload_cubemap(hg_ctx* ctx, int32_t face_size, int32_t n_mips, const float* texels, size_t n_floats);
+
+int hg_set_params(hg_ctx* ctx, const hg_params* params);
+
+/* (Re)allocate the accumulation target for a width x height image and clear it (OnCameraSetup). */
+int hg_resize(hg_ctx* ctx, int32_t width, int32_t height);
+
+/* Multi-GPU: this context renders only the 8x8 tiles t with t % n_ranks == rank (tile-row-major order). */
+int hg_set_tiling(hg_ctx* ctx, int32_t rank, int32_t n_ranks);
+
+int hg_clear_accumulation(hg_ctx* ctx);
+
+/* Trace n_frames consecutive frames, FrameCount = params.frameCount + k, each followed by the
+ * progressive blend acc = acc*(1-w) + new*w with w = 1.0f/FrameCount (AccumulationShader.shader:33).
+ * accumulate == 0 reproduces Accumulate=false: FrameCount forced to 1 and acc = new each frame.
+ * Asynchronous on the context stream. */
+int hg_render(hg_ctx* ctx, int32_t n_frames, int32_t accumulate);
+
+int hg_synchronize(hg_ctx* ctx);
+
+/* Row-major RGBA32F image (width*height*4 floats) of the accumulation target.  With tiling, only this
+ * rank's pixels are written; the others are left untouched. Blocks. */
+int hg_readback(hg_ctx* ctx, float* rgba, size_t n_floats);
+
+/* Device-to-device copy of this rank's packed tiles (n_local_tiles * 64 * 4 floats, tile-major,
+ * pixel (lx,ly) of a tile at lx + 8*ly) into caller-owned device memory on the same device. */
+int hg_copy_tiles_device(hg_ctx* ctx, void* dst_device, size_t n_bytes);
+int32_t hg_local_tile_count(const hg_ctx* ctx);
+
+int hg_get_counters(const hg_ctx* ctx, hg_counters* out);
+int hg_reset_counters(hg_ctx* ctx);
+
+/* Tuning knobs (kernel variant, block size, counters on/off). */
+int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
+
+/* ----------------------------------------------------------------------------------------------
+ * Host-side data producers (the reference keeps these in C#: BVHGenerator.cs, RayTracingMesh.cs,
+ * HalogenRenderPass.UpdateObjectBuffers).  Restated in C++ with the reference's float semantics,
+ * so a non-Unity caller can build the buffers hg_upload_scene takes.
+ * -------------------------------------------------------------------------------------------- */
+
+/* BVHGenerator.GenerateMeshBVH (BVHGenerator.cs:13-134).  `indices` (3*n_tris) is REORDERED IN PLACE,
+ * exactly as the reference reorders its triangle list.  root_min/root_max = Unity mesh.bounds.min/max.
+ * Writes at most max_nodes entries; returns the node count (or a negative error / the required count
+ * negated-minus-one if max_nodes is too small). */
+int64_t hg_build_blas(const float* vertices, int32_t n_vertices, int32_t* indices, int32_t n_tris,
+                      const float root_min[3], const float root_max[3], int32_t max_hierarchy_depth,
+                      BVHEntry* out_nodes, int64_t max_nodes);
+
+/* Unity Bounds.SetMinMax(min,max) followed by .min/.max (centre/extents round trip) — the arithmetic
+ * every bound in the reference goes through (BVHGenerator.cs:171-183, RayTracingMesh.cs:106-117). */
+void hg_unity_bounds(const float in_min[3], const float in_max[3], int32_t pad_if_thin,
+                     float out_min[3], float out_max[3]);
+
+/* RayTracingMesh.UpdateTriangleList (RayTracingMesh.cs:70-87). */
+int hg_pack_triangles(const float* vertices, const float* normals, int32_t n_vertices,
+                      const int32_t* indices, int32_t n_tris, HalogenTriangle* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HALOGEN_ABI_H */
