@@ -1,26 +1,10 @@
-// hg_trace.hip — the Halogen path-tracing megakernel for gfx950 (CDNA4, wave64).
+// hg_device.h — device-side building blocks of the Halogen hot path shared by the kernels
+// (hg_mega.hip: one-thread-per-pixel megakernel; hg_wavefront.hip: regenerating wavefront pipeline).
 //
-// Reference: Assets/Scripts/Halogen Shaders/HalgoenCompute.compute (kernel HalogenCompute, :1015-1063)
-//            Assets/Scripts/Halogen Shaders/HalogenRandom.hlsl   (sampler)
-//            Assets/Scripts/Halogen Shaders/AccumulationShader.shader:27-34 (fused here as the epilogue)
-//
-// Execution model (MI355X-first, not a translation of the [numthreads(8,8,1)] HLSL dispatch):
-//   * one wave64 = one 8x8 pixel tile; a 256-thread workgroup = 4 tiles.  Tiles are dealt to ranks
-//     round-robin (multi-GPU) and the accumulation buffer is tile-major, so each wave reads and writes
-//     one contiguous KiB of float4.
-//   * each lane runs n_frames frames of its pixel back to back (FrameCount = first .. first+n-1) and
-//     keeps the progressive average in registers: the accumulation "blit" of the reference becomes the
-//     kernel epilogue, and the 16-B accumulator crosses HBM once per launch instead of 3x per frame.
-//   * BLAS traversal uses a per-lane stack in LDS laid out [depth][lane] (lane-contiguous, conflict-free
-//     ds_read/write_b32), child-pair node records (hg_layout.h) and pre-subtracted triangle edges.
-//   * the Owen-scrambled Sobol sampler uses closed forms of the two Sobol dimensions the reference uses:
-//     sobol(i, 0) = bitreverse(i) and sobol(i, 1) = bitreverse(superset-XOR-transform(i)), so
-//     owen_scramble(sobol(i,d), s) = bitreverse(LK(·, s)) needs no 32-iteration loop; bit-exact with
-//     the reference's table loop (tests/test_sampler_closed_form.py, and the GPU parity tests).
-//   * all fp arithmetic follows the reference's operation order with -ffp-contract=off and the shared
-//     spec include/hg_fmath.h, so results are bit-identical to the CPU oracle.
-//   * per-lane work counters (TriangleTests / AABBTests of the reference, rays, hits) are reduced per
-//     wave with DPP/permute shuffles and added with one 64-bit atomic per wave per counter.
+// Every function restates a piece of the reference (file:line in its comment) in the reference's
+// operation order, compiled with -ffp-contract=off and the shared arithmetic spec include/hg_fmath.h, so the
+// results are bit-identical to the CPU oracle.
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include "hg_fmath.h"
@@ -28,7 +12,7 @@
 
 #pragma clang fp contract(off)
 
-namespace {
+namespace hgd {
 
 // ---------------------------------------------------------------------------------------------------
 // float3 helpers with the reference's evaluation order (no FMA)
@@ -642,73 +626,5 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-}  // namespace
+}  // namespace hgd
 
-template <bool kCounters>
-__global__ __launch_bounds__(256) void hg_trace_kernel(const HgKernelParams kp) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
-    const int gtile = kp.rank + local_tile * kp.n_ranks;
-    const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-    const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-    const bool active = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu;
-    Counters c{0, 0, 0, 0, 0, 0};
-    uint32_t paths = 0;
-    if (active) {
-        uint32_t* stack = lds_stack + threadIdx.x;
-        const uint32_t stride = blockDim.x;
-        const size_t slot = size_t(local_tile) * 64 + lane;
-        float4 acc = kp.acc[slot];
-        // HalogenCompute :1023-1033
-        const float ndcx = (float(px) / kp.W) * 2.0f - 1.0f;
-        const float ndcy = (float(py) / kp.H) * 2.0f - 1.0f;
-        const uint32_t pixel_id = pcg_hash(px + py * kp.Wu);
-        for (int f = 0; f < kp.n_frames; ++f) {
-            const int32_t fc = kp.accumulate ? kp.first_frame + f : 1;
-            Sampler smp{uint32_t(fc), pixel_id, 0u};
-            MediumStack ms{0ull, 0};
-            f3 color = mk(0, 0, 0);
-            for (uint32_t s = 0; s < kp.spp; ++s) {
-                const Ray r = camera_ray(kp, smp, ndcx, ndcy);
-                paths++;
-                if (kp.debug_mode < 1) color = color + trace_ray(kp, smp, ms, r, c, stack, stride);
-                else color = color + trace_ray_debug(kp, smp, ms, r, c, stack, stride);
-            }
-            const float sppf = float(kp.spp);
-            color = mk(color.x / sppf, color.y / sppf, color.z / sppf);
-            if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                const float w = 1.0f / float(fc);
-                const float k = 1.0f - w;
-                acc.x = acc.x * k + color.x * w;
-                acc.y = acc.y * k + color.y * w;
-                acc.z = acc.z * k + color.z * w;
-                acc.w = acc.w * k + 1.0f * w;
-            } else {
-                acc = make_float4(color.x, color.y, color.z, 1.0f);
-            }
-        }
-        kp.acc[slot] = acc;
-    }
-    if (kCounters) {
-        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.meshes, c.spheres, c.hits};
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const uint32_t s = wave_sum(v[k]);
-            if (lane == 0 && s) atomicAdd(kp.counters + k, (unsigned long long)s);
-        }
-    }
-}
-
-// Launcher used by the runtime (hg_runtime.hip)
-hipError_t hg_launch_trace(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
-    const int tiles_per_block = block / 64;
-    const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
-    if (grid == 0) return hipSuccess;
-    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
-    if (counters)
-        hipLaunchKernelGGL(hg_trace_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
-    else
-        hipLaunchKernelGGL(hg_trace_kernel<false>, dim3(grid), dim3(block), lds, stream, kp);
-    return hipGetLastError();
-}

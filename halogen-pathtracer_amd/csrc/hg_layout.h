@@ -73,4 +73,21 @@ struct HgKernelParams {
     // outputs
     float4* __restrict__ acc;
     unsigned long long* __restrict__ counters;  // 7 x u64, order of hg_counters' first 7 fields
+
+    // wavefront pipeline state (hg_wavefront.hip), SoA, one entry per local pixel slot
+    // (slot = local_tile*64 + lane, the same index as the tile-major accumulation buffer)
+    uint32_t n_slots;
+    float4* __restrict__ p_o;    // ray origin xyz, accumulated roughness (trace_ray's accumulatedRoughnes)
+    float4* __restrict__ p_d;    // ray direction xyz
+    float4* __restrict__ p_thr;  // lightAttenuation xyz
+    float4* __restrict__ p_col;  // accumulatedColor of the current sample xyz
+    float4* __restrict__ p_sum;  // RayColor: sum over the samples of the current frame
+    uint4* __restrict__ p_st;    // bounceTypes[0..2], rayInteractions
+    uint4* __restrict__ p_st2;   // SobolDimensionOffset, sample index, frame index, medium stack pointer
+    uint2* __restrict__ p_ms;    // medium stack: 8 material indices, one byte each
+    float4* __restrict__ h_tuvo; // hit: t, barycentric u, v, orientation
+    uint2* __restrict__ h_id;    // hit: primitive (triangle index | sphere index + HG_SPHERE_BIT | HG_NONE), mesh
 };
+
+#define HG_NONE 0xFFFFFFFFu
+#define HG_SPHERE_BIT 0x80000000u

@@ -19,7 +19,13 @@
 #include "hg_fmath.h"
 #include "hg_layout.h"
 
-hipError_t hg_launch_trace(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
+hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
+                              const uint32_t* n_in, uint32_t* head, hipStream_t s);
+hipError_t hg_wf_launch_shade(const HgKernelParams& kp, int grid, const uint32_t* q_in, const uint32_t* n_in,
+                              uint32_t* q_out, uint32_t* n_out, hipStream_t s);
+int hg_wf_trace_blocks_per_cu(int block, size_t lds_bytes);
 
 namespace {
 
@@ -56,13 +62,21 @@ struct hg_ctx {
     int32_t W = 0, H = 0, rank = 0, n_ranks = 1, tiles_x = 0, tiles_y = 0, n_local_tiles = 0;
     DevBuf acc;
 
+    // wavefront pipeline state (hg_wavefront.hip), sized for the local pixel slots
+    DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
+    DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
+    uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
+    size_t poll_cap = 0;
+    std::vector<hipEvent_t> poll_events;
+
     // counters / timing
     DevBuf counters_dev;
     hg_counters counters{};
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events, pending_trace;
 
-    // options
-    int32_t kernel = HG_KERNEL_MEGA, block = 256, counters_on = 1;
+    // device / options
+    int n_cu = 0;
+    int32_t kernel = HG_KERNEL_WAVEFRONT, block = 128, counters_on = 1, timing = 0;
 };
 
 namespace {
@@ -111,7 +125,7 @@ float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 float bits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
 int drain_events(hg_ctx* c) {
-    if (c->pending.empty()) return HG_OK;
+    if (c->pending.empty() && c->pending_trace.empty()) return HG_OK;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     for (auto& pr : c->pending) {
         float ms = 0.0f;
@@ -119,7 +133,36 @@ int drain_events(hg_ctx* c) {
         c->counters.kernel_ms += double(ms);
         c->free_events.push_back(pr);
     }
+    for (auto& pr : c->pending_trace) {
+        float ms = 0.0f;
+        HG_HIP(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+        c->counters.trace_ms += double(ms);
+        c->counters.trace_launches++;
+        c->free_events.push_back(pr);
+    }
     c->pending.clear();
+    c->pending_trace.clear();
+    return HG_OK;
+}
+
+int event_pair(hg_ctx* c, std::pair<hipEvent_t, hipEvent_t>& ev) {
+    if (!c->free_events.empty()) {
+        ev = c->free_events.back();
+        c->free_events.pop_back();
+        return HG_OK;
+    }
+    HG_HIP(c, hipEventCreate(&ev.first));
+    HG_HIP(c, hipEventCreate(&ev.second));
+    return HG_OK;
+}
+
+int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 16);
+    if (b.bytes >= bytes) return HG_OK;
+    release(b);
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    b.bytes = bytes;
     return HG_OK;
 }
 
@@ -129,12 +172,88 @@ int alloc_target(hg_ctx* c) {
     const int64_t total = int64_t(c->tiles_x) * c->tiles_y;
     c->n_local_tiles = total > c->rank ? int32_t((total - c->rank + c->n_ranks - 1) / c->n_ranks) : 0;
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
+    const size_t slots = size_t(c->n_local_tiles) * 64;
+    for (DevBuf* b : {&c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col, &c->wf_sum, &c->wf_tuvo})
+        if (int rc = ensure(c, *b, slots * sizeof(float4))) return rc;
+    for (DevBuf* b : {&c->wf_st, &c->wf_st2})
+        if (int rc = ensure(c, *b, slots * sizeof(uint4))) return rc;
+    for (DevBuf* b : {&c->wf_ms, &c->wf_id})
+        if (int rc = ensure(c, *b, slots * sizeof(uint2))) return rc;
+    for (DevBuf* b : {&c->wf_q0, &c->wf_q1})
+        if (int rc = ensure(c, *b, slots * sizeof(uint32_t))) return rc;
     release(c->acc);
     if (bytes) {
         hipError_t e = hipMalloc(&c->acc.p, bytes);
         if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipMalloc(accumulation %zu) failed", bytes);
         c->acc.bytes = bytes;
         HG_HIP(c, hipMemsetAsync(c->acc.p, 0, bytes, c->stream));
+    }
+    return HG_OK;
+}
+
+
+// The bounce loop of the wavefront pipeline: gen, then (trace, shade) per iteration until the queue is empty.
+// The host does not wait for queue lengths: it launches ahead and polls pinned copies of the lengths a few
+// iterations behind, stopping once one of them reads zero (an empty queue stays empty).
+int render_wavefront(hg_ctx* c, const HgKernelParams& kp) {
+    const uint64_t max_iter64 = uint64_t(kp.n_frames) * kp.spp * (uint64_t(kp.max_bounces) + 1u);
+    if (max_iter64 > (1ull << 30)) return fail(c, HG_E_UNSUPPORTED, "n_frames * spp * (maxBounces+1) too large");
+    const size_t L = size_t(max_iter64);
+    if (int rc = ensure(c, c->wf_counts, (L + 1) * sizeof(uint32_t))) return rc;
+    if (int rc = ensure(c, c->wf_heads, L * sizeof(uint32_t))) return rc;
+    const size_t n_polls = L / 4 + 2;
+    if (c->poll_cap < n_polls) {
+        if (c->poll_host) (void)hipHostFree(c->poll_host);
+        c->poll_host = nullptr;
+        HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->poll_host), n_polls * sizeof(uint32_t), 0));
+        c->poll_cap = n_polls;
+    }
+    while (c->poll_events.size() < 8) {
+        hipEvent_t e;
+        HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->poll_events.push_back(e);
+    }
+    uint32_t* counts = static_cast<uint32_t*>(c->wf_counts.p);
+    uint32_t* heads = static_cast<uint32_t*>(c->wf_heads.p);
+    uint32_t* q[2] = {static_cast<uint32_t*>(c->wf_q0.p), static_cast<uint32_t*>(c->wf_q1.p)};
+    HG_HIP(c, hipMemsetAsync(counts, 0, (L + 1) * sizeof(uint32_t), c->stream));
+    HG_HIP(c, hipMemsetAsync(heads, 0, L * sizeof(uint32_t), c->stream));
+    hipError_t e = hg_wf_launch_gen(kp, q[0], counts, c->stream);
+    if (e != hipSuccess) return fail(c, HG_E_HIP, "gen launch failed: %s", hipGetErrorString(e));
+
+    const int block = c->block;
+    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    const int bpc = hg_wf_trace_blocks_per_cu(block, lds);
+    const int trace_grid = std::max(1, bpc * c->n_cu);
+    const int shade_grid = int(std::max<size_t>(1, std::min<size_t>((kp.n_slots + 255) / 256, size_t(c->n_cu) * 8)));
+    const size_t POLL = 4;  // poll every 4 iterations, read back two polls behind
+    size_t polls = 0;
+    for (size_t it = 0; it < L; ++it) {
+        std::pair<hipEvent_t, hipEvent_t> tev;
+        if (c->timing) {
+            if (int rc = event_pair(c, tev)) return rc;
+            HG_HIP(c, hipEventRecord(tev.first, c->stream));
+        }
+        e = hg_wf_launch_trace(kp, trace_grid, block, kp.counters != nullptr, q[it & 1], counts + it, heads + it,
+                               c->stream);
+        if (e != hipSuccess) return fail(c, HG_E_HIP, "trace launch failed: %s", hipGetErrorString(e));
+        if (c->timing) {
+            HG_HIP(c, hipEventRecord(tev.second, c->stream));
+            c->pending_trace.push_back(tev);
+        }
+        e = hg_wf_launch_shade(kp, shade_grid, q[it & 1], counts + it, q[(it + 1) & 1], counts + it + 1, c->stream);
+        if (e != hipSuccess) return fail(c, HG_E_HIP, "shade launch failed: %s", hipGetErrorString(e));
+        if (it % POLL == POLL - 1 && it + 1 < L) {
+            HG_HIP(c, hipMemcpyAsync(c->poll_host + polls, counts + it + 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     c->stream));
+            HG_HIP(c, hipEventRecord(c->poll_events[polls % c->poll_events.size()], c->stream));
+            ++polls;
+            if (polls >= 3) {  // check the poll issued two polls ago (normally complete by now)
+                const size_t k = polls - 3;
+                hipEvent_t pe = c->poll_events[k % c->poll_events.size()];
+                if (hipEventQuery(pe) == hipSuccess && c->poll_host[k] == 0) break;
+            }
+        }
     }
     return HG_OK;
 }
@@ -159,6 +278,12 @@ int hg_create(int device, hg_ctx** out) {
         return HG_E_HIP;
     }
     c->counters_dev.bytes = 16 * sizeof(unsigned long long);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        delete c;
+        return HG_E_HIP;
+    }
+    c->n_cu = prop.multiProcessorCount;
     if (hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes) != hipSuccess) {
         delete c;
         return HG_E_HIP;
@@ -172,8 +297,13 @@ void hg_destroy(hg_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
-                      &c->normals, &c->cube, &c->acc, &c->counters_dev})
+                      &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
+                      &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
+                      &c->wf_counts, &c->wf_heads})
         release(*b);
+    if (c->poll_host) (void)hipHostFree(c->poll_host);
+    for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
+    for (auto& pr : c->pending_trace) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->free_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -433,24 +563,37 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.acc = static_cast<float4*>(c->acc.p);
     kp.counters = static_cast<unsigned long long*>(c->counters_dev.p);
 
+    kp.n_slots = uint32_t(c->n_local_tiles) * 64u;
+    kp.p_o = static_cast<float4*>(c->wf_o.p);
+    kp.p_d = static_cast<float4*>(c->wf_d.p);
+    kp.p_thr = static_cast<float4*>(c->wf_thr.p);
+    kp.p_col = static_cast<float4*>(c->wf_col.p);
+    kp.p_sum = static_cast<float4*>(c->wf_sum.p);
+    kp.p_st = static_cast<uint4*>(c->wf_st.p);
+    kp.p_st2 = static_cast<uint4*>(c->wf_st2.p);
+    kp.p_ms = static_cast<uint2*>(c->wf_ms.p);
+    kp.h_tuvo = static_cast<float4*>(c->wf_tuvo.p);
+    kp.h_id = static_cast<uint2*>(c->wf_id.p);
+    if (!c->counters_on) kp.counters = nullptr;
+
     std::pair<hipEvent_t, hipEvent_t> ev;
-    if (!c->free_events.empty()) {
-        ev = c->free_events.back();
-        c->free_events.pop_back();
-    } else {
-        HG_HIP(c, hipEventCreate(&ev.first));
-        HG_HIP(c, hipEventCreate(&ev.second));
-    }
+    if (int rc = event_pair(c, ev)) return rc;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
-    hipError_t e = hg_launch_trace(kp, c->block, c->counters_on != 0, c->stream);
-    if (e != hipSuccess) {
+    const bool mega = c->kernel == HG_KERNEL_MEGA || p.halogenDebugMode != 0;
+    if (mega) {
+        hipError_t e = hg_launch_mega(kp, c->block == 128 ? 256 : c->block, c->counters_on != 0, c->stream);
+        if (e != hipSuccess) {
+            c->free_events.push_back(ev);
+            return fail(c, HG_E_HIP, "megakernel launch failed: %s", hipGetErrorString(e));
+        }
+    } else if (int rc = render_wavefront(c, kp)) {
         c->free_events.push_back(ev);
-        return fail(c, HG_E_HIP, "trace kernel launch failed: %s", hipGetErrorString(e));
+        return rc;
     }
     HG_HIP(c, hipEventRecord(ev.second, c->stream));
     c->pending.push_back(ev);
     c->counters.launches++;
-    if (c->pending.size() > 256) {
+    if (c->pending.size() + c->pending_trace.size() > 4096) {
         if (int rc = drain_events(c)) return rc;
     }
     if (accumulate) c->params.frameCount += n_frames;  // FrameCount++ per accumulated frame (RP:347)
@@ -536,7 +679,8 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
     switch (option) {
         case HG_OPT_KERNEL:
-            if (value != HG_KERNEL_MEGA) return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
+            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT)
+                return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
             c->kernel = value;
             return HG_OK;
         case HG_OPT_BLOCK:
@@ -545,6 +689,9 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             return HG_OK;
         case HG_OPT_COUNTERS:
             c->counters_on = value ? 1 : 0;
+            return HG_OK;
+        case HG_OPT_TIMING:
+            c->timing = value ? 1 : 0;
             return HG_OK;
         default:
             return fail(c, HG_E_INVALID, "unknown option %d", option);

@@ -76,15 +76,16 @@ class HgParams(C.Structure):  # every uniform of HalgoenCompute.compute:26-68,18
 class HgCounters(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
-                ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64)]
+                ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
+                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 HG_OK = 0
-HG_KERNEL_MEGA, HG_KERNEL_PERSISTENT = 0, 1
-HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS = 1, 2, 3
+HG_KERNEL_MEGA, HG_KERNEL_WAVEFRONT = 0, 1
+HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING = 1, 2, 3, 4
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [

@@ -139,8 +139,10 @@ typedef struct hg_counters {
     uint64_t mesh_visits;  /* rays x meshes (world->local transforms) */
     uint64_t sphere_tests; /* rays x spheres (sphere AABB prefilters) */
     uint64_t hits;         /* accepted hits (hit.rayT < far) */
-    double kernel_ms;      /* summed device time of the trace kernel (HIP events on the context stream) */
-    uint64_t launches;     /* trace kernel launches */
+    double kernel_ms;      /* summed device time of whole hg_render dispatches (HIP events on the context stream) */
+    uint64_t launches;     /* hg_render dispatches timed in kernel_ms */
+    double trace_ms;       /* summed device time of the traversal kernel alone (only with HG_OPT_TIMING on) */
+    uint64_t trace_launches; /* traversal kernel launches timed in trace_ms */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -155,9 +157,13 @@ enum {
     HG_E_UNSUPPORTED = -6
 };
 
-/* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v). */
-enum { HG_KERNEL_MEGA = 0, HG_KERNEL_PERSISTENT = 1 };
-enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3 };
+/* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v).  WAVEFRONT (default): regenerating
+ * gen/trace/shade pipeline with compacted ray queues.  MEGA: one thread per pixel for all frames (always used for
+ * the debug views 1-5). */
+enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1 };
+/* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
+ * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms). */
+enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4 };
 
 int hg_abi_version(void);
 

@@ -96,7 +96,8 @@ def make_scene(packed, cubemap=None) -> tuple[HgoScene, list]:
 class Counters(C.Structure):  # hg_counters layout
     _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
-                ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64)]
+                ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
+                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

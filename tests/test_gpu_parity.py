@@ -15,9 +15,16 @@ GOLD = Path(__file__).resolve().parent / "golden"
 REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a diagnostic, the test is bitwise
 
 
-def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None):
+KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA}
+
+
+def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
+               block=None):
     own = ctx is None
     ctx = ctx or abi.Context(0)
+    ctx.set_option(abi.HG_OPT_KERNEL, KERNELS[kernel])
+    if block:
+        ctx.set_option(abi.HG_OPT_BLOCK, block)
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)
     ctx.upload_scene(packed)
     if cube is not None:
@@ -47,25 +54,30 @@ def assert_bitwise(got, want, what=""):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("name", sorted(cases.CASES))
-def test_gpu_matches_golden(gpu, name):
+def test_gpu_matches_golden(gpu, name, kernel):
     meta = json.loads((GOLD / f"{name}.json").read_text())
     packed, params, cube, frames, acc = cases.setup(name)
     assert cases.packed_digest(packed) == meta["scene_sha256"]
-    img, cnt = gpu_render(packed, params, frames, acc, cube)
+    img, cnt = gpu_render(packed, params, frames, acc, cube, kernel=kernel)
     assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], name)
     for k, v in meta["counters"].items():
         assert cnt[k] == v, (k, cnt[k], v)
 
 
 @pytest.mark.gpu
-def test_gpu_frame_splits_and_tiling(gpu):
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_gpu_frame_splits_and_tiling(gpu, kernel):
     packed, params, cube, frames, acc = cases.setup("c1_64")
-    ref, _ = gpu_render(packed, params, 4)
-    img, _ = gpu_render(packed, params, 4, splits=[1, 3])
+    ref, _ = gpu_render(packed, params, 4, kernel=kernel)
+    img, _ = gpu_render(packed, params, 4, splits=[1, 3], kernel=kernel)
     assert_bitwise(img, ref, "1+3 frames")
+    for block in (64, 256):
+        img, _ = gpu_render(packed, params, 4, kernel=kernel, block=block)
+        assert_bitwise(img, ref, f"block {block}")
     for n_ranks in (2, 3, 8):
-        parts = [gpu_render(packed, params, 4, tiling=(r, n_ranks))[0] for r in range(n_ranks)]
+        parts = [gpu_render(packed, params, 4, tiling=(r, n_ranks), kernel=kernel)[0] for r in range(n_ranks)]
         merged = np.full_like(ref, np.nan)
         for p in parts:
             m = ~np.isnan(p)
@@ -74,8 +86,9 @@ def test_gpu_frame_splits_and_tiling(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("cfg_name,rows", [("C3", (536, 540)), ("C2", (0, 4)), ("C5", (700, 703))])
-def test_gpu_full_size_rows_match_oracle(gpu, cfg_name, rows):
+def test_gpu_full_size_rows_match_oracle(gpu, cfg_name, rows, kernel):
     """BASELINE-sized configs (1080p; C3 with the full 871,200-triangle dragon): a band of rows traced by the
     oracle must equal the same rows of the GPU image, bit for bit."""
     cfg = scenes.CONFIGS[cfg_name]
@@ -85,7 +98,7 @@ def test_gpu_full_size_rows_match_oracle(gpu, cfg_name, rows):
     cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
     frames = 2
-    img, _ = gpu_render(packed, params, frames, True, cube)
+    img, _ = gpu_render(packed, params, frames, True, cube, kernel=kernel)
     W = cfg.width
     y0, y1 = rows
     ref, _ = hg_oracle.render(packed, params, frames, True, cubemap=cube, pix_range=(y0 * W, y1 * W))
