@@ -85,6 +85,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--kernel", default="wavefront", choices=["wavefront", "mega"])
+    ap.add_argument("--frames-per-step", type=int, default=1,
+                    help="progressive frames per hg_render call per GPU-equivalent (semantics unchanged)")
+    ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
+    ap.add_argument("--refill", type=int, default=0)
     ap.add_argument("--no-counters", action="store_true")
     ap.add_argument("--save-image", default="")
     args = ap.parse_args()
@@ -116,6 +121,11 @@ def main():
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
 
     ctx = abi.Context(local_rank)
+    ctx.set_option(abi.HG_OPT_KERNEL, abi.HG_KERNEL_WAVEFRONT if args.kernel == "wavefront" else abi.HG_KERNEL_MEGA)
+    if args.timing:
+        ctx.set_option(abi.HG_OPT_TIMING, 1)
+    if args.refill:
+        ctx.set_option(abi.HG_OPT_REFILL, args.refill)
     if args.block:
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
     if args.no_counters:
@@ -128,7 +138,7 @@ def main():
     ctx.set_params(params)
     setup_s = time.perf_counter() - t_setup
 
-    frames_per_step = world  # per-GPU work fixed: one frame-equivalent of the image per GPU per step
+    frames_per_step = world * args.frames_per_step  # per-GPU work fixed: frame-equivalents of the image per GPU
     for _ in range(args.warmup):
         ctx.render(frames_per_step, True)
     ctx.synchronize()
@@ -218,6 +228,8 @@ def main():
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "setup_s": setup_s,
+            "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
+                          "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},
             "cpu_baseline": None,
         }
         if args.save_image:

@@ -28,9 +28,10 @@
 #define HG_LEAF_BIT 0x80000000u
 #define HG_TILE 8
 #define HG_MAX_CUBE_MIPS 16
+#define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
 
-struct HgDevMesh {
-    float w2l[16];
+struct alignas(16) HgDevMesh {
+    float w2l[16];  // Unity column-major: column c = w2l[4c .. 4c+3]
     uint32_t root_ref;
     uint32_t tri_offset;
     uint32_t material;
@@ -56,6 +57,9 @@ struct HgKernelParams {
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
+    uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
+    uint32_t* __restrict__ spill;  // wavefront trace: per-lane stack entries beyond HG_LDS_STACK (rarely touched)
+    uint32_t spill_stride;          // = threads of the persistent trace grid
     // cubemap
     int32_t cube_size, cube_mips;
     uint32_t cube_mip_offset[HG_MAX_CUBE_MIPS];  // in float4 texels

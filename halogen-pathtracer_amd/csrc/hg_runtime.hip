@@ -26,6 +26,8 @@ hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, boo
 hipError_t hg_wf_launch_shade(const HgKernelParams& kp, int grid, const uint32_t* q_in, const uint32_t* n_in,
                               uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 int hg_wf_trace_blocks_per_cu(int block, size_t lds_bytes);
+size_t hg_wf_trace_lds_bytes(uint32_t stack_depth, int block);
+int64_t hg_wf_selftest_rcp(int64_t* tested);
 
 namespace {
 
@@ -65,6 +67,7 @@ struct hg_ctx {
     // wavefront pipeline state (hg_wavefront.hip), sized for the local pixel slots
     DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
     DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
+    DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -76,7 +79,7 @@ struct hg_ctx {
 
     // device / options
     int n_cu = 0;
-    int32_t kernel = HG_KERNEL_WAVEFRONT, block = 128, counters_on = 1, timing = 0;
+    int32_t kernel = HG_KERNEL_WAVEFRONT, block = 128, counters_on = 1, timing = 0, refill = 32;
 };
 
 namespace {
@@ -222,9 +225,15 @@ int render_wavefront(hg_ctx* c, const HgKernelParams& kp) {
     if (e != hipSuccess) return fail(c, HG_E_HIP, "gen launch failed: %s", hipGetErrorString(e));
 
     const int block = c->block;
-    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    const size_t lds = hg_wf_trace_lds_bytes(kp.stack_depth, block);
     const int bpc = hg_wf_trace_blocks_per_cu(block, lds);
     const int trace_grid = std::max(1, bpc * c->n_cu);
+    HgKernelParams kpt = kp;
+    kpt.spill_stride = uint32_t(trace_grid) * uint32_t(block);
+    if (kp.stack_depth > HG_LDS_STACK) {
+        if (int rc = ensure(c, c->wf_spill, size_t(kpt.spill_stride) * (kp.stack_depth - HG_LDS_STACK) * 4)) return rc;
+        kpt.spill = static_cast<uint32_t*>(c->wf_spill.p);
+    }
     const int shade_grid = int(std::max<size_t>(1, std::min<size_t>((kp.n_slots + 255) / 256, size_t(c->n_cu) * 8)));
     const size_t POLL = 4;  // poll every 4 iterations, read back two polls behind
     size_t polls = 0;
@@ -234,7 +243,7 @@ int render_wavefront(hg_ctx* c, const HgKernelParams& kp) {
             if (int rc = event_pair(c, tev)) return rc;
             HG_HIP(c, hipEventRecord(tev.first, c->stream));
         }
-        e = hg_wf_launch_trace(kp, trace_grid, block, kp.counters != nullptr, q[it & 1], counts + it, heads + it,
+        e = hg_wf_launch_trace(kpt, trace_grid, block, kp.counters != nullptr, q[it & 1], counts + it, heads + it,
                                c->stream);
         if (e != hipSuccess) return fail(c, HG_E_HIP, "trace launch failed: %s", hipGetErrorString(e));
         if (c->timing) {
@@ -299,7 +308,7 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -547,6 +556,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.n_ranks = c->n_ranks;
     kp.n_local_tiles = c->n_local_tiles;
     kp.stack_depth = c->stack_depth;
+    kp.refill_min = uint32_t(c->refill);
     kp.cube_size = c->cube_size;
     kp.cube_mips = c->cube_mips;
     std::memcpy(kp.cube_mip_offset, c->cube_mip_offset, sizeof kp.cube_mip_offset);
@@ -675,6 +685,15 @@ int hg_reset_counters(hg_ctx* c) {
     return HG_OK;
 }
 
+int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = set_device(c)) return rc;
+    if (test != HG_SELFTEST_RCP) return fail(c, HG_E_INVALID, "unknown self-test %d", test);
+    const int64_t r = hg_wf_selftest_rcp(tested);
+    if (r < 0) return fail(c, HG_E_HIP, "self-test failed to run");
+    return r;
+}
+
 int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
     switch (option) {
@@ -692,6 +711,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             return HG_OK;
         case HG_OPT_TIMING:
             c->timing = value ? 1 : 0;
+            return HG_OK;
+        case HG_OPT_REFILL:
+            if (value < 1 || value > 64) return fail(c, HG_E_INVALID, "refill must be 1..64");
+            c->refill = value;
             return HG_OK;
         default:
             return fail(c, HG_E_INVALID, "unknown option %d", option);

@@ -114,31 +114,67 @@ __global__ __launch_bounds__(256) void hg_wf_gen(const HgKernelParams kp, uint32
 // ---------------------------------------------------------------------------------------------------------
 namespace {
 enum : uint32_t { ST_IDLE = 0, ST_MESH = 1, ST_TRAV = 2 };
+
+// Traversal stack: the first HG_LDS_STACK entries of each lane live in LDS ([depth][lane], conflict-free), deeper
+// entries (rare: the BLAS depth cap is 32) spill to a per-lane global array, so the LDS footprint stays small
+// enough for full occupancy.
+struct Stack {
+    uint32_t* lds;    // this lane's LDS column
+    uint32_t lds_stride;
+    uint32_t* spill;  // this lane's spill column
+    uint32_t spill_stride;
+    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
+        if (sp < HG_LDS_STACK) lds[sp * lds_stride] = v;
+        else spill[(sp - HG_LDS_STACK) * spill_stride] = v;
+        ++sp;
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const {
+        --sp;
+        return sp < HG_LDS_STACK ? lds[sp * lds_stride] : spill[(sp - HG_LDS_STACK) * spill_stride];
+    }
+};
+
+// 1/x, correctly rounded (what the reference's `1 / det`, `1 / dir` compute in IEEE fp32).  With HG_FAST_RCP the
+// hardware reciprocal (<= 1 ulp) is refined by one FMA Newton step, which is correctly rounded for every x whose
+// exponent keeps x and 1/x normal (checked for all 2^32 inputs by hg_selftest / tests/test_gpu_selftest.py);
+// zeros, denormals, huge values, infinities and NaNs take the IEEE division.
+__device__ __forceinline__ float rcp_exact(float x) {
+#if HG_FAST_RCP
+    const uint32_t ex = (__float_as_uint(x) >> 23) & 0xFFu;
+    if (__builtin_expect(ex - 2u <= 250u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, r, 1.0f);
+        return __builtin_fmaf(e, r, r);
+    }
+#endif
+    return 1.0f / x;
 }
+}  // namespace
 
 template <bool kCounters>
-__global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, const uint32_t* __restrict__ q_in,
+__global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKernelParams kp, const uint32_t* __restrict__ q_in,
                                                    const uint32_t* __restrict__ n_in, uint32_t* __restrict__ head) {
     extern __shared__ uint32_t lds_stack[];
-    uint32_t* const stack = lds_stack + threadIdx.x;
-    const uint32_t stride = blockDim.x;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    const Stack stk{lds_stack + threadIdx.x, blockDim.x, kp.spill + gtid, kp.spill_stride};
     const uint32_t n = *n_in;
     const float eps = 0.0001f;
 
-    uint32_t c_rays = 0, c_tri = 0, c_aabb = 0, c_mesh = 0, c_sph = 0;
+    uint32_t c_rays = 0, c_tri = 0, c_aabb = 0;
     uint32_t st = ST_IDLE;
     bool exhausted = false;
     uint32_t slot = 0, mi = 0, node = HG_NONE, sp = 0;
-    f3 wo = mk(0, 0, 0), wd = mk(0, 0, 0), lo = mk(0, 0, 0), ld = mk(0, 0, 0), inv = mk(0, 0, 0);
-    float best_t = HG_INF, best_u = 0.0f, best_v = 0.0f, best_o = 0.0f, sph_t = HG_INF, sph_o = 0.0f;
-    uint32_t best_tri = HG_NONE, best_mesh = 0, sph_i = HG_NONE;
+    f3 lo = mk(0, 0, 0), ld = mk(0, 0, 0), inv = mk(0, 0, 0);
+    float best_t = HG_INF, best_u = 0.0f, best_v = 0.0f, sph_t = HG_INF;
+    uint32_t best_tri = HG_NONE, best_mesh = 0, sph_io = HG_NONE;  // sph_io: sphere index | orientation<0 << 31
 
     for (;;) {
         // ---- refill idle lanes (wave-aggregated dequeue) ----
         {
             const bool want = st == ST_IDLE && !exhausted;
             const uint64_t m = __ballot(want);
-            if (m) {
+            // batch dequeues: one atomic per >= refill_min rays keeps the shared head word far from saturation
+            if (m && (uint32_t(__popcll(m)) >= kp.refill_min || !__any(st != ST_IDLE))) {
                 const uint32_t lane = lane_id();
                 const int leader = __ffsll((unsigned long long)m) - 1;
                 uint32_t base = 0;
@@ -149,18 +185,16 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
                     if (idx < n) {
                         slot = q_in[idx];
                         const float4 o4 = kp.p_o[slot], d4 = kp.p_d[slot];
-                        wo = mk(o4.x, o4.y, o4.z);
-                        wd = mk(d4.x, d4.y, d4.z);
+                        const f3 wo = mk(o4.x, o4.y, o4.z), wd = mk(d4.x, d4.y, d4.z);
                         c_rays++;
                         // get_ray_scene_intersection_sphere :357-376
-                        const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+                        const f3 winv = mk(rcp_exact(wd.x), rcp_exact(wd.y), rcp_exact(wd.z));
                         sph_t = HG_INF;
-                        sph_i = HG_NONE;
+                        sph_io = HG_NONE;
                         for (int i = 0; i < kp.n_spheres; ++i) {
                             const float4 cr = kp.spheres[3 * i];
                             const float4 am = kp.spheres[3 * i + 1];
                             const float4 bb = kp.spheres[3 * i + 2];
-                            c_sph++;
                             if (!(ray_aabb(xyz(am), xyz(bb), wo, winv) < kp.far_)) continue;
                             const f3 sh = wo - xyz(cr);
                             const float bq = 2.0f * dot(sh, wd);
@@ -168,15 +202,14 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
                             const float disc = bq * bq - 4.0f * cq;
                             if (!(disc >= 0.0f)) continue;
                             float hd = (-bq - __builtin_sqrtf(disc)) / 2.0f;
-                            float orient = 1.0f;
+                            uint32_t back = 0;
                             if (hd < 0.0f) {
                                 hd = (-bq + __builtin_sqrtf(disc)) / 2.0f;
-                                orient = -1.0f;
+                                back = 0x80000000u;
                             }
                             if (hd < sph_t && hd > eps) {
                                 sph_t = hd;
-                                sph_o = orient;
-                                sph_i = uint32_t(i);
+                                sph_io = uint32_t(i) | back;
                             }
                         }
                         best_t = sph_t;  // closestIntersection.rayT = closestHit.rayT (:381)
@@ -194,17 +227,19 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
         // ---- mesh setup / ray finish ----
         if (st == ST_MESH) {
             if (mi < uint32_t(kp.n_meshes)) {
-                const HgDevMesh& md = kp.meshes[mi];
-                const float* m = md.w2l;
-                c_mesh++;
-                lo = mk(((m[0] * wo.x + m[4] * wo.y) + m[8] * wo.z) + m[12] * 1.0f,
-                        ((m[1] * wo.x + m[5] * wo.y) + m[9] * wo.z) + m[13] * 1.0f,
-                        ((m[2] * wo.x + m[6] * wo.y) + m[10] * wo.z) + m[14] * 1.0f);
-                ld = mk(((m[0] * wd.x + m[4] * wd.y) + m[8] * wd.z) + m[12] * 0.0f,
-                        ((m[1] * wd.x + m[5] * wd.y) + m[9] * wd.z) + m[13] * 0.0f,
-                        ((m[2] * wd.x + m[6] * wd.y) + m[10] * wd.z) + m[14] * 0.0f);
-                inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
-                node = md.root_ref;  // root pushed untested (:401), held in a register
+                const float4* md = reinterpret_cast<const float4*>(kp.meshes + mi);
+                const float4 c0 = md[0], c1 = md[1], c2 = md[2], c3 = md[3];  // worldToLocal columns
+                const uint32_t root = __float_as_uint(md[4].x);
+                const float4 o4 = kp.p_o[slot], d4 = kp.p_d[slot];  // world ray (L1/L2-resident)
+                // mul(worldToLocal, float4(o,1)) / float4(d,0), direction NOT normalized (:390-392)
+                lo = mk(((c0.x * o4.x + c1.x * o4.y) + c2.x * o4.z) + c3.x * 1.0f,
+                        ((c0.y * o4.x + c1.y * o4.y) + c2.y * o4.z) + c3.y * 1.0f,
+                        ((c0.z * o4.x + c1.z * o4.y) + c2.z * o4.z) + c3.z * 1.0f);
+                ld = mk(((c0.x * d4.x + c1.x * d4.y) + c2.x * d4.z) + c3.x * 0.0f,
+                        ((c0.y * d4.x + c1.y * d4.y) + c2.y * d4.z) + c3.y * 0.0f,
+                        ((c0.z * d4.x + c1.z * d4.y) + c2.z * d4.z) + c3.z * 0.0f);
+                inv = mk(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
+                node = root;  // root pushed untested (:401), held in a register
                 sp = 0;
                 st = ST_TRAV;
             } else {
@@ -212,11 +247,11 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
                 float4 tuvo;
                 uint2 id;
                 if (best_t < (sph_t - eps) && best_t < kp.far_) {
-                    tuvo = make_float4(best_t, best_u, best_v, best_o);
-                    id = make_uint2(best_tri, best_mesh);
-                } else if (sph_i != HG_NONE) {
-                    tuvo = make_float4(sph_t, 0.0f, 0.0f, sph_o);
-                    id = make_uint2(sph_i | HG_SPHERE_BIT, 0u);
+                    tuvo = make_float4(best_t, best_u, best_v, __uint_as_float(0x3F800000u | (best_tri & 0x80000000u)));
+                    id = make_uint2(best_tri & 0x7FFFFFFFu, best_mesh);
+                } else if (sph_io != HG_NONE) {
+                    tuvo = make_float4(sph_t, 0.0f, 0.0f, (sph_io & 0x80000000u) ? -1.0f : 1.0f);
+                    id = make_uint2((sph_io & 0x7FFFFFFFu) | HG_SPHERE_BIT, 0u);
                 } else {
                     tuvo = make_float4(HG_INF, 0.0f, 0.0f, 0.0f);
                     id = make_uint2(HG_NONE, 0u);
@@ -241,49 +276,54 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
                 const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
                 const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
                 if (nearOk) {
-                    if (farOk) stack[(sp++) * stride] = farRef;
+                    if (farOk) stk.push(sp, farRef);
                     node = nearRef;
                 } else if (farOk) {
                     node = farRef;
                 } else {
-                    node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
+                    node = sp > 0 ? stk.pop(sp) : HG_NONE;
                 }
             }
         }
 
-        // ---- one leaf per lane ----
+        // ---- one leaf per lane: triangles tested branch-free, the next one's loads issued ahead ----
         if (st == ST_TRAV && node != HG_NONE) {
             const uint2 leaf = kp.leaves[node & ~HG_LEAF_BIT];
-            for (uint32_t k = 0; k < leaf.y; ++k) {
-                const uint32_t ti = leaf.x + k;
-                const float4 ta = kp.tri_a[ti];
-                const float4 tb = kp.tri_b[ti];
-                const float tc = kp.tri_c[ti];
+            uint32_t ti = leaf.x;
+            const uint32_t end = leaf.x + leaf.y;
+            float4 ta = kp.tri_a[ti], tb = kp.tri_b[ti];
+            float tc = kp.tri_c[ti];
+            for (; ti < end; ++ti) {
+                const float4 a = ta, b = tb;
+                const float cz = tc;
+                if (ti + 1 < end) {
+                    ta = kp.tri_a[ti + 1];
+                    tb = kp.tri_b[ti + 1];
+                    tc = kp.tri_c[ti + 1];
+                }
                 c_tri++;
-                // triangle_intersection_doublesided :307-355
-                const f3 e1 = mk(ta.w, tb.x, tb.y);
-                const f3 e2 = mk(tb.z, tb.w, tc);
+                // triangle_intersection_doublesided :307-355 (all terms computed, one combined accept)
+                const f3 e1 = mk(a.w, b.x, b.y);
+                const f3 e2 = mk(b.z, b.w, cz);
                 const f3 pvec = cross(ld, e2);
                 const float det = dot(pvec, e1);
-                if (fabsf(det) < 0.00000001f) continue;
-                const float inv_det = 1.0f / det;
-                const f3 tvec = lo - xyz(ta);
+                const float inv_det = rcp_exact(det);
+                const f3 tvec = lo - xyz(a);
                 const float U = dot(tvec, pvec) * inv_det;
-                if (U < 0.0f || U > 1.0f) continue;
                 const f3 qvec = cross(tvec, e1);
                 const float V = dot(ld, qvec) * inv_det;
-                if (V < 0.0f || U + V > 1.0f) continue;
                 const float t = dot(e2, qvec) * inv_det;
-                if (t > 0.0f && t > eps && t < best_t) {
+                const bool ok = !(fabsf(det) < 0.00000001f) && !(U < 0.0f || U > 1.0f) && !(V < 0.0f || U + V > 1.0f) &&
+                                t > 0.0f && t > eps && t < best_t;
+                if (ok) {
                     best_t = t;
                     best_u = U;
                     best_v = V;
-                    best_o = det > 0.0f ? 1.0f : -1.0f;
-                    best_tri = ti;
+                    best_tri = ti | (det > 0.0f ? 0u : 0x80000000u);  // orientation = sign(det)
                     best_mesh = mi;
                 }
             }
-            node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
+            node = sp > 0 ? stk.pop(sp) : HG_NONE;
         }
         if (st == ST_TRAV && node == HG_NONE) {
             mi++;
@@ -291,7 +331,9 @@ __global__ __launch_bounds__(256) void hg_wf_trace(const HgKernelParams kp, cons
         }
     }
     if (kCounters) {
-        const uint32_t v[7] = {0, c_rays, c_tri, c_aabb, c_mesh, c_sph, 0};
+        // every ray visits every mesh and tests every sphere prefilter: those counts follow from c_rays
+        const uint32_t v[7] = {0, c_rays, c_tri, c_aabb, c_rays * uint32_t(kp.n_meshes),
+                               c_rays * uint32_t(kp.n_spheres), 0};
         wave_add_counters(kp, v);
     }
 }
@@ -446,9 +488,13 @@ hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t*
     return hipGetLastError();
 }
 
+size_t hg_wf_trace_lds_bytes(uint32_t stack_depth, int block) {
+    return size_t(std::min<uint32_t>(stack_depth, HG_LDS_STACK)) * size_t(block) * sizeof(uint32_t);
+}
+
 hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
                               const uint32_t* n_in, uint32_t* head, hipStream_t s) {
-    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    const size_t lds = hg_wf_trace_lds_bytes(kp.stack_depth, block);
     if (counters)
         hipLaunchKernelGGL(hg_wf_trace<true>, dim3(grid), dim3(block), lds, s, kp, q_in, n_in, head);
     else
@@ -466,4 +512,37 @@ int hg_wf_trace_blocks_per_cu(int block, size_t lds_bytes) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hg_wf_trace<true>, block, lds_bytes) != hipSuccess) return 1;
     return n > 0 ? n : 1;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// self-test: the fast reciprocal path against IEEE division for all 2^32 inputs of its range
+// ---------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hg_selftest_rcp_kernel(unsigned long long* mismatches, unsigned long long* tested) {
+    unsigned long long bad = 0, cnt = 0;
+    for (uint64_t u = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; u < (1ull << 32);
+         u += uint64_t(gridDim.x) * blockDim.x) {
+        const float x = __uint_as_float(uint32_t(u));
+        const uint32_t ex = (uint32_t(u) >> 23) & 0xFFu;
+        if (ex - 2u > 250u) continue;
+        const float r = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, r, 1.0f);
+        const float fast = __builtin_fmaf(e, r, r);
+        const float ref = 1.0f / x;
+        bad += __float_as_uint(fast) != __float_as_uint(ref);
+        cnt++;
+    }
+    atomicAdd(mismatches, bad);
+    atomicAdd(tested, cnt);
+}
+
+int64_t hg_wf_selftest_rcp(int64_t* tested) {
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    hipLaunchKernelGGL(hg_selftest_rcp_kernel, dim3(8192), dim3(256), 0, 0, d, d + 1);
+    unsigned long long h[2] = {0, 0};
+    if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    (void)hipFree(d);
+    if (tested) *tested = int64_t(h[1]);
+    return int64_t(h[0]);
 }

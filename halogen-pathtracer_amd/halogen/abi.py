@@ -13,7 +13,8 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libhalogen_hip.so"
+# HALOGEN_LIB selects an alternative build of the same library (A/B variants in tools/sweep.sh)
+LIB_PATH = Path(os.environ["HALOGEN_LIB"]) if os.environ.get("HALOGEN_LIB") else _HERE / "libhalogen_hip.so"
 
 
 class Vec3(C.Structure):
@@ -85,15 +86,16 @@ class HgCounters(C.Structure):
 
 HG_OK = 0
 HG_KERNEL_MEGA, HG_KERNEL_WAVEFRONT = 0, 1
-HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING = 1, 2, 3, 4
+HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING, HG_OPT_REFILL = 1, 2, 3, 4, 5
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [
     "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
     "hg_readback", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
-    "hg_set_option", "hg_build_blas", "hg_unity_bounds", "hg_pack_triangles",
+    "hg_set_option", "hg_selftest", "hg_build_blas", "hg_unity_bounds", "hg_pack_triangles",
 ]
+HG_SELFTEST_RCP = 1
 
 _lib = None
 
@@ -127,6 +129,7 @@ def lib() -> C.CDLL:
         "hg_get_counters": (C.c_int, [P, C.POINTER(HgCounters)]),
         "hg_reset_counters": (C.c_int, [P]),
         "hg_set_option": (C.c_int, [P, i32, i32]),
+        "hg_selftest": (i64, [P, i32, C.POINTER(i64)]),
         "hg_build_blas": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64]),
         "hg_unity_bounds": (None, [f32p, f32p, i32, f32p, f32p]),
         "hg_pack_triangles": (C.c_int, [P, P, i32, P, i32, P]),
@@ -241,6 +244,14 @@ class Context:
 
     def set_option(self, option: int, value: int) -> None:
         self._check(lib().hg_set_option(self._h, option, value), "hg_set_option")
+
+    def selftest(self, test: int = HG_SELFTEST_RCP) -> tuple[int, int]:
+        """(mismatches, inputs tested) of a device arithmetic self-test."""
+        tested = C.c_int64(0)
+        r = lib().hg_selftest(self._h, test, C.byref(tested))
+        if r < 0:
+            self._check(int(r), "hg_selftest")
+        return int(r), int(tested.value)
 
 
 def gpu_available() -> bool:

@@ -162,8 +162,9 @@ enum {
  * the debug views 1-5). */
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
- * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms). */
-enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4 };
+ * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
+ * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64). */
+enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5 };
 
 int hg_abi_version(void);
 
@@ -218,6 +219,12 @@ int hg_reset_counters(hg_ctx* ctx);
 
 /* Tuning knobs (kernel variant, block size, counters on/off). */
 int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
+
+/* Device self-tests of arithmetic shortcuts the kernels rely on.  HG_SELFTEST_RCP: the fast correctly-rounded
+ * reciprocal against IEEE 1.0f/x for every float of its range.  Returns the number of mismatches (must be 0),
+ * or a negative error; *tested (optional) receives the number of inputs checked. */
+enum { HG_SELFTEST_RCP = 1 };
+int64_t hg_selftest(hg_ctx* ctx, int32_t test, int64_t* tested);
 
 /* ----------------------------------------------------------------------------------------------
  * Host-side data producers (the reference keeps these in C#: BVHGenerator.cs, RayTracingMesh.cs,
