@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="wavefront", choices=["wavefront", "mega"])
+    ap.add_argument("--kernel", default="mega", choices=["wavefront", "mega"])
     ap.add_argument("--frames-per-step", type=int, default=1,
                     help="progressive frames per hg_render call per GPU-equivalent (semantics unchanged)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")

@@ -150,6 +150,22 @@ __device__ __forceinline__ int32_t mat_priority(const HgKernelParams& kp, uint32
 // ---------------------------------------------------------------------------------------------------
 // Intersection (:244-485)
 // ---------------------------------------------------------------------------------------------------
+// 1/x, correctly rounded (the reference's `1 / det`, `1 / dir` in IEEE fp32).  With HG_FAST_RCP the hardware
+// reciprocal (<= 1 ulp) is refined by one FMA Newton step, correctly rounded for every x whose exponent keeps x
+// and 1/x normal (checked for all 2^32 inputs by hg_selftest, tests/test_gpu_selftest.py); zeros, denormals,
+// huge values, infinities and NaNs take the IEEE division.
+__device__ __forceinline__ float rcp_exact(float x) {
+#if HG_FAST_RCP
+    const uint32_t ex = (__float_as_uint(x) >> 23) & 0xFFu;
+    if (__builtin_expect(ex - 2u <= 250u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, r, 1.0f);
+        return __builtin_fmaf(e, r, r);
+    }
+#endif
+    return 1.0f / x;
+}
+
 __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-259
     f3 t1 = (A - o) * inv;
     f3 t2 = (B - o) * inv;
@@ -164,7 +180,7 @@ __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-2
 
 __device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c) {  // :357-376
     float closest = h.t;
-    f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    f3 inv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     for (int i = 0; i < kp.n_spheres; ++i) {
         const float4 cr = kp.spheres[3 * i];
         const float4 am = kp.spheres[3 * i + 1];
@@ -195,91 +211,143 @@ __device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, 
     }
 }
 
+// Exact mesh skip (HgDevMesh::cull_*): bit m of the result is clear when the ray certainly misses both children of
+// mesh m's root in the reference's local-space test, or meets them only beyond `best_t` — the reference would test
+// those two boxes, push nothing and find nothing there.  Meshes >= 64 are never culled.
+__device__ __forceinline__ uint64_t mesh_live_mask(const HgKernelParams& kp, f3 wo, f3 winv, float best_t,
+                                                   uint32_t& culled) {
+    uint64_t live = ~0ull;
+    const float lim = best_t * 1.0001f + 1e-4f;
+    const int ncull = kp.n_meshes < 64 ? kp.n_meshes : 64;
+    for (int m = 0; m < ncull; ++m) {
+        const HgDevMesh& md = kp.meshes[m];
+        if (!md.cullable) continue;
+        const float dA = ray_aabb(xyz(md.cull_a_lo), xyz(md.cull_a_hi), wo, winv);
+        const float dB = ray_aabb(xyz(md.cull_b_lo), xyz(md.cull_b_hi), wo, winv);
+        const bool farA = dA == HG_INF || dA > lim, farB = dB == HG_INF || dB > lim;  // NaN never skips
+        if (farA && farB) {
+            live &= ~(1ull << m);
+            culled++;
+        }
+    }
+    return live;
+}
+
+// Triangle test of triangle_intersection_doublesided (:307-355) with every term computed and one combined accept
+// (same values as the early-out form).  Returns true when the hit is accepted as the new closest (:416).
+__device__ __forceinline__ bool tri_accept(f3 lo, f3 ld, float4 a, float4 b, float cz, float best_t, float& t,
+                                           float& U, float& V, bool& front) {
+    const f3 e1 = mk(a.w, b.x, b.y);
+    const f3 e2 = mk(b.z, b.w, cz);
+    const f3 pvec = cross(ld, e2);
+    const float det = dot(pvec, e1);
+    const float inv_det = rcp_exact(det);
+    const f3 tvec = lo - xyz(a);
+    U = dot(tvec, pvec) * inv_det;
+    const f3 qvec = cross(tvec, e1);
+    V = dot(ld, qvec) * inv_det;
+    t = dot(e2, qvec) * inv_det;
+    front = det > 0.0f;
+    return !(fabsf(det) < 0.00000001f) && !(U < 0.0f || U > 1.0f) && !(V < 0.0f || U + V > 1.0f) && t > 0.0f &&
+           t > 0.0001f && t < best_t;
+}
+
 // get_ray_scene_intersection_mesh, :378-472.  `stack` points at this lane's column of the LDS stack.
+// The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
+// the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
+// while-while: all lanes descend inner nodes together until each holds a leaf, then test one leaf each.
 __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, uint32_t* stack,
                              uint32_t stride) {
     const float eps = 0.0001f;
     float best_t = h.t;  // closestIntersection.rayT starts at the sphere hit (:381)
-    float best_u = 0.0f, best_v = 0.0f, best_o = 0.0f;
-    uint32_t best_tri = 0xFFFFFFFFu;  // global triangle index
+    float best_u = 0.0f, best_v = 0.0f;
+    uint32_t best_tri = HG_NONE;  // global triangle index | (orientation < 0) << 31
     int best_mesh = -1;
+    uint32_t culled = 0;
+    const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
+    const uint64_t live = mesh_live_mask(kp, ray.o, winv, best_t, culled);
+    c.aabb += 2 * culled;
+    c.meshes += uint32_t(kp.n_meshes);
     for (int mi = 0; mi < kp.n_meshes; ++mi) {
-        const HgDevMesh& md = kp.meshes[mi];
-        c.meshes++;
-        // world -> local, direction NOT normalized (:390-392); md.w2l is Unity column-major: M(r,c)=w2l[c*4+r]
-        const float* m = md.w2l;
-        f3 lo = mk(((m[0] * ray.o.x + m[4] * ray.o.y) + m[8] * ray.o.z) + m[12] * 1.0f,
-                   ((m[1] * ray.o.x + m[5] * ray.o.y) + m[9] * ray.o.z) + m[13] * 1.0f,
-                   ((m[2] * ray.o.x + m[6] * ray.o.y) + m[10] * ray.o.z) + m[14] * 1.0f);
-        f3 ld = mk(((m[0] * ray.d.x + m[4] * ray.d.y) + m[8] * ray.d.z) + m[12] * 0.0f,
-                   ((m[1] * ray.d.x + m[5] * ray.d.y) + m[9] * ray.d.z) + m[13] * 0.0f,
-                   ((m[2] * ray.d.x + m[6] * ray.d.y) + m[10] * ray.d.z) + m[14] * 0.0f);
-        f3 inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
-        uint32_t sp = 0;
-        stack[0] = md.root_ref;  // root pushed untested (:401)
-        sp = 1;
-        while (sp > 0) {
-            const uint32_t ref = stack[(--sp) * stride];
-            if (ref & HG_LEAF_BIT) {
-                const uint2 leaf = kp.leaves[ref & ~HG_LEAF_BIT];
-                for (uint32_t k = 0; k < leaf.y; ++k) {
-                    const uint32_t ti = leaf.x + k;
-                    const float4 ta = kp.tri_a[ti];
-                    const float4 tb = kp.tri_b[ti];
-                    const float tc = kp.tri_c[ti];
+        bool active = mi >= 64 || ((live >> mi) & 1ull);
+        if (!__any(active)) continue;  // the whole wave skips this mesh
+        if (!active) continue;
+        const float4* md4 = reinterpret_cast<const float4*>(kp.meshes + mi);
+        const float4 c0 = md4[0], c1 = md4[1], c2 = md4[2], c3 = md4[3];  // worldToLocal columns
+        const uint32_t root = __float_as_uint(md4[4].x);
+        // world -> local, direction NOT normalized (:390-392)
+        const f3 lo = mk(((c0.x * ray.o.x + c1.x * ray.o.y) + c2.x * ray.o.z) + c3.x * 1.0f,
+                         ((c0.y * ray.o.x + c1.y * ray.o.y) + c2.y * ray.o.z) + c3.y * 1.0f,
+                         ((c0.z * ray.o.x + c1.z * ray.o.y) + c2.z * ray.o.z) + c3.z * 1.0f);
+        const f3 ld = mk(((c0.x * ray.d.x + c1.x * ray.d.y) + c2.x * ray.d.z) + c3.x * 0.0f,
+                         ((c0.y * ray.d.x + c1.y * ray.d.y) + c2.y * ray.d.z) + c3.y * 0.0f,
+                         ((c0.z * ray.d.x + c1.z * ray.d.y) + c2.z * ray.d.z) + c3.z * 0.0f);
+        const f3 inv = mk(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
+        uint32_t node = root, sp = 0;  // root pushed untested (:401), held in a register
+        while (__any(active)) {
+            while (__any(active && !(node & HG_LEAF_BIT))) {
+                if (active && !(node & HG_LEAF_BIT)) {
+                    const float4* rec = kp.nodes + 4 * node;
+                    const float4 a_lo = rec[0], a_hi = rec[1], b_lo = rec[2], b_hi = rec[3];
+                    const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
+                    const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                    c.aabb += 2;
+                    const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                    // reference (:430-444): push far, push near (each only if tEntry < closest), pop near
+                    const bool bFirst = dB < dA;
+                    const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
+                    const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
+                    if (nearOk) {
+                        if (farOk) stack[(sp++) * stride] = farRef;
+                        node = nearRef;
+                    } else if (farOk) {
+                        node = farRef;
+                    } else {
+                        node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
+                    }
+                }
+            }
+            if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
+                const uint2 leaf = kp.leaves[node & ~HG_LEAF_BIT];
+                uint32_t ti = leaf.x;
+                const uint32_t end = leaf.x + leaf.y;
+                float4 ta = kp.tri_a[ti], tb = kp.tri_b[ti];
+                float tc = kp.tri_c[ti];
+                for (; ti < end; ++ti) {
+                    const float4 a = ta, b = tb;
+                    const float cz = tc;
+                    if (ti + 1 < end) {
+                        ta = kp.tri_a[ti + 1];
+                        tb = kp.tri_b[ti + 1];
+                        tc = kp.tri_c[ti + 1];
+                    }
                     c.tri++;
-                    // triangle_intersection_doublesided :307-355
-                    const f3 e1 = mk(ta.w, tb.x, tb.y);
-                    const f3 e2 = mk(tb.z, tb.w, tc);
-                    const f3 pvec = cross(ld, e2);
-                    const float det = dot(pvec, e1);
-                    if (fabsf(det) < 0.00000001f) continue;
-                    const float inv_det = 1.0f / det;
-                    const f3 tvec = lo - xyz(ta);
-                    const float U = dot(tvec, pvec) * inv_det;
-                    if (U < 0.0f || U > 1.0f) continue;
-                    const f3 qvec = cross(tvec, e1);
-                    const float V = dot(ld, qvec) * inv_det;
-                    if (V < 0.0f || U + V > 1.0f) continue;
-                    const float t = dot(e2, qvec) * inv_det;
-                    if (!(t > 0.0f)) continue;
-                    if (t > eps && t < best_t) {
+                    float t, U, V;
+                    bool front;
+                    if (tri_accept(lo, ld, a, b, cz, best_t, t, U, V, front)) {
                         best_t = t;
                         best_u = U;
                         best_v = V;
-                        best_o = det > 0.0f ? 1.0f : -1.0f;
-                        best_tri = ti;
+                        best_tri = ti | (front ? 0u : 0x80000000u);
                         best_mesh = mi;
                     }
                 }
-            } else {
-                const float4* rec = kp.nodes + 4 * (ref);
-                const float4 a_lo = rec[0], a_hi = rec[1], b_lo = rec[2], b_hi = rec[3];
-                const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
-                const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
-                c.aabb += 2;
-                const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
-                // push the farther child first so the nearer is popped first (:430-444)
-                if (dB < dA) {
-                    if (dA < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refA;
-                    if (dB < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refB;
-                } else {
-                    if (dB < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refB;
-                    if (dA < best_t && sp < kp.stack_depth) stack[(sp++) * stride] = refA;
-                }
+                node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
             }
+            if (node == HG_NONE) active = false;
         }
     }
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
         const HgDevMesh& md = kp.meshes[best_mesh];
+        const uint32_t tri = best_tri & 0x7FFFFFFFu;
+        const float orient = (best_tri & 0x80000000u) ? -1.0f : 1.0f;
         h.t = best_t;
         h.mat = md.material;
-        h.orient = best_o;
-        const float4 n0 = kp.normals[3 * best_tri], d1 = kp.normals[3 * best_tri + 1],
-                     d2 = kp.normals[3 * best_tri + 2];
+        h.orient = orient;
+        const float4 n0 = kp.normals[3 * tri], d1 = kp.normals[3 * tri + 1], d2 = kp.normals[3 * tri + 2];
         f3 n = (xyz(n0) + xyz(d1) * best_u) + xyz(d2) * best_v;
-        n = n * best_o;
+        n = n * orient;
         // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform)
         const float* m = md.w2l;
         f3 w = mk(((n.x * m[0] + n.y * m[1]) + n.z * m[2]) + 0.0f * m[3],

@@ -35,7 +35,12 @@ struct alignas(16) HgDevMesh {
     uint32_t root_ref;
     uint32_t tri_offset;
     uint32_t material;
-    uint32_t pad;
+    uint32_t cullable;  // 1: the root is an inner node and cull_* hold its children's padded world boxes
+    // World-space boxes of the root's two children, padded far beyond every float rounding of the reference's
+    // local-space test (hg_runtime.hip: mesh_cull_boxes).  If a ray certainly misses both (or meets them only
+    // beyond its current closest hit), the reference's traversal of this mesh would test exactly those two
+    // boxes, push nothing and find nothing — so the mesh is skipped and only its 2 AABB tests are counted.
+    float4 cull_a_lo, cull_a_hi, cull_b_lo, cull_b_hi;
 };
 
 // Everything the trace kernel needs, passed by value as the kernel argument.

@@ -13,7 +13,7 @@
 using namespace hgd;
 
 template <bool kCounters>
-__global__ __launch_bounds__(256) void hg_trace_kernel(const HgKernelParams kp) {
+__global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x & 63u;
     const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);

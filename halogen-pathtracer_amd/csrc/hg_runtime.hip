@@ -79,7 +79,7 @@ struct hg_ctx {
 
     // device / options
     int n_cu = 0;
-    int32_t kernel = HG_KERNEL_WAVEFRONT, block = 128, counters_on = 1, timing = 0, refill = 32;
+    int32_t kernel = HG_KERNEL_MEGA, block = 128, counters_on = 1, timing = 0, refill = 32;
 };
 
 namespace {
@@ -126,6 +126,82 @@ int upload(hg_ctx* c, DevBuf& b, const void* src, size_t bytes) {
 float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 float bits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+// Padded world-space boxes of a mesh root's two children (for the exact mesh skip in hg_wavefront.hip).
+// The local box corners go through the double-precision inverse of the float worldToLocal the kernel uses;
+// the pad (1e-3 of the box size + 1e-4 of the coordinate magnitude + 1e-5) exceeds by orders of magnitude
+// the float rounding of the reference's local-space slab test (~1e-7 relative), so "misses the padded box"
+// implies "the reference's ray_AABB_test returns INF (or a tEntry beyond the closest hit)".
+bool invert4(const double a[16], double out[16]) {
+    double inv[16];
+    inv[0] = a[5] * a[10] * a[15] - a[5] * a[11] * a[14] - a[9] * a[6] * a[15] + a[9] * a[7] * a[14] +
+             a[13] * a[6] * a[11] - a[13] * a[7] * a[10];
+    inv[4] = -a[4] * a[10] * a[15] + a[4] * a[11] * a[14] + a[8] * a[6] * a[15] - a[8] * a[7] * a[14] -
+             a[12] * a[6] * a[11] + a[12] * a[7] * a[10];
+    inv[8] = a[4] * a[9] * a[15] - a[4] * a[11] * a[13] - a[8] * a[5] * a[15] + a[8] * a[7] * a[13] +
+             a[12] * a[5] * a[11] - a[12] * a[7] * a[9];
+    inv[12] = -a[4] * a[9] * a[14] + a[4] * a[10] * a[13] + a[8] * a[5] * a[14] - a[8] * a[6] * a[13] -
+              a[12] * a[5] * a[10] + a[12] * a[6] * a[9];
+    inv[1] = -a[1] * a[10] * a[15] + a[1] * a[11] * a[14] + a[9] * a[2] * a[15] - a[9] * a[3] * a[14] -
+             a[13] * a[2] * a[11] + a[13] * a[3] * a[10];
+    inv[5] = a[0] * a[10] * a[15] - a[0] * a[11] * a[14] - a[8] * a[2] * a[15] + a[8] * a[3] * a[14] +
+             a[12] * a[2] * a[11] - a[12] * a[3] * a[10];
+    inv[9] = -a[0] * a[9] * a[15] + a[0] * a[11] * a[13] + a[8] * a[1] * a[15] - a[8] * a[3] * a[13] -
+             a[12] * a[1] * a[11] + a[12] * a[3] * a[9];
+    inv[13] = a[0] * a[9] * a[14] - a[0] * a[10] * a[13] - a[8] * a[1] * a[14] + a[8] * a[2] * a[13] +
+              a[12] * a[1] * a[10] - a[12] * a[2] * a[9];
+    inv[2] = a[1] * a[6] * a[15] - a[1] * a[7] * a[14] - a[5] * a[2] * a[15] + a[5] * a[3] * a[14] +
+             a[13] * a[2] * a[7] - a[13] * a[3] * a[6];
+    inv[6] = -a[0] * a[6] * a[15] + a[0] * a[7] * a[14] + a[4] * a[2] * a[15] - a[4] * a[3] * a[14] -
+             a[12] * a[2] * a[7] + a[12] * a[3] * a[6];
+    inv[10] = a[0] * a[5] * a[15] - a[0] * a[7] * a[13] - a[4] * a[1] * a[15] + a[4] * a[3] * a[13] +
+              a[12] * a[1] * a[7] - a[12] * a[3] * a[5];
+    inv[14] = -a[0] * a[5] * a[14] + a[0] * a[6] * a[13] + a[4] * a[1] * a[14] - a[4] * a[2] * a[13] -
+              a[12] * a[1] * a[6] + a[12] * a[2] * a[5];
+    inv[3] = -a[1] * a[6] * a[11] + a[1] * a[7] * a[10] + a[5] * a[2] * a[11] - a[5] * a[3] * a[10] -
+             a[9] * a[2] * a[7] + a[9] * a[3] * a[6];
+    inv[7] = a[0] * a[6] * a[11] - a[0] * a[7] * a[10] - a[4] * a[2] * a[11] + a[4] * a[3] * a[10] +
+             a[8] * a[2] * a[7] - a[8] * a[3] * a[6];
+    inv[11] = -a[0] * a[5] * a[11] + a[0] * a[7] * a[9] + a[4] * a[1] * a[11] - a[4] * a[3] * a[9] -
+              a[8] * a[1] * a[7] + a[8] * a[3] * a[5];
+    inv[15] = a[0] * a[5] * a[10] - a[0] * a[6] * a[9] - a[4] * a[1] * a[10] + a[4] * a[2] * a[9] +
+              a[8] * a[1] * a[6] - a[8] * a[2] * a[5];
+    const double det = a[0] * inv[0] + a[1] * inv[4] + a[2] * inv[8] + a[3] * inv[12];
+    if (!(std::fabs(det) > 1e-30) || !std::isfinite(det)) return false;
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] / det;
+    return true;
+}
+
+bool world_box(const double l2w[16], const BVHEntry& e, float4& lo, float4& hi) {
+    const float c[2][3] = {{e.boundingCornerA.x, e.boundingCornerA.y, e.boundingCornerA.z},
+                           {e.boundingCornerB.x, e.boundingCornerB.y, e.boundingCornerB.z}};
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    for (int k = 0; k < 8; ++k) {
+        const double p[3] = {c[k & 1][0], c[(k >> 1) & 1][1], c[(k >> 2) & 1][2]};
+        for (int r = 0; r < 3; ++r) {  // column-major: M(r,col) = l2w[col*4 + r]
+            const double w = l2w[r] * p[0] + l2w[4 + r] * p[1] + l2w[8 + r] * p[2] + l2w[12 + r];
+            if (!std::isfinite(w)) return false;
+            mn[r] = std::min(mn[r], w);
+            mx[r] = std::max(mx[r], w);
+        }
+    }
+    double size = 0.0, mag = 0.0;
+    for (int r = 0; r < 3; ++r) {
+        size = std::max(size, mx[r] - mn[r]);
+        mag = std::max({mag, std::fabs(mn[r]), std::fabs(mx[r])});
+    }
+    const double pad = 1e-3 * size + 1e-4 * mag + 1e-5;
+    lo = make_float4(float(mn[0] - pad), float(mn[1] - pad), float(mn[2] - pad), 0.0f);
+    hi = make_float4(float(mx[0] + pad), float(mx[1] + pad), float(mx[2] + pad), 0.0f);
+    return true;
+}
+
+bool mesh_cull_boxes(const hg_mat4& w2l, const BVHEntry& A, const BVHEntry& B, HgDevMesh& dm) {
+    double a[16], l2w[16];
+    for (int i = 0; i < 16; ++i) a[i] = w2l.m[i];
+    if (!invert4(a, l2w)) return false;
+    return world_box(l2w, A, dm.cull_a_lo, dm.cull_a_hi) && world_box(l2w, B, dm.cull_b_lo, dm.cull_b_hi);
+}
 
 int drain_events(hg_ctx* c) {
     if (c->pending.empty() && c->pending_trace.empty()) return HG_OK;
@@ -423,7 +499,12 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
         dm[mi].root_ref = ref_of(off);
         dm[mi].tri_offset = toff;
         dm[mi].material = m.materialIndex;
-        dm[mi].pad = 0;
+        dm[mi].cullable = 0;
+        if (blas[off].triangleCount == 0) {
+            const BVHEntry& A = blas[off + blas[off].indexA];
+            const BVHEntry& B = blas[off + blas[off].indexA + 1];
+            if (mesh_cull_boxes(m.worldToLocal, A, B, dm[mi])) dm[mi].cullable = 1;
+        }
     }
     c->stack_depth = std::max<uint32_t>(2u, (max_depth + 2 + 1) & ~1u);
 

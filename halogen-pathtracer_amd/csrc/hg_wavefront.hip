@@ -134,21 +134,13 @@ struct Stack {
     }
 };
 
-// 1/x, correctly rounded (what the reference's `1 / det`, `1 / dir` compute in IEEE fp32).  With HG_FAST_RCP the
-// hardware reciprocal (<= 1 ulp) is refined by one FMA Newton step, which is correctly rounded for every x whose
-// exponent keeps x and 1/x normal (checked for all 2^32 inputs by hg_selftest / tests/test_gpu_selftest.py);
-// zeros, denormals, huge values, infinities and NaNs take the IEEE division.
-__device__ __forceinline__ float rcp_exact(float x) {
-#if HG_FAST_RCP
-    const uint32_t ex = (__float_as_uint(x) >> 23) & 0xFFu;
-    if (__builtin_expect(ex - 2u <= 250u, 1)) {
-        const float r = __builtin_amdgcn_rcpf(x);
-        const float e = __builtin_fmaf(-x, r, 1.0f);
-        return __builtin_fmaf(e, r, r);
-    }
-#endif
-    return 1.0f / x;
+// first mesh index >= m that is not culled (meshes beyond 64 carry no cull bit and are always visited)
+__device__ __forceinline__ uint32_t next_live(uint64_t live, uint32_t m) {
+    if (m >= 64u) return m;
+    const uint64_t b = live & (~0ull << m);
+    return b ? uint32_t(__builtin_ctzll(b)) : 64u;
 }
+
 }  // namespace
 
 template <bool kCounters>
@@ -167,6 +159,7 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
     f3 lo = mk(0, 0, 0), ld = mk(0, 0, 0), inv = mk(0, 0, 0);
     float best_t = HG_INF, best_u = 0.0f, best_v = 0.0f, sph_t = HG_INF;
     uint32_t best_tri = HG_NONE, best_mesh = 0, sph_io = HG_NONE;  // sph_io: sphere index | orientation<0 << 31
+    uint64_t live = ~0ull;  // meshes < 64 not skipped by the exact cull (meshes >= 64 are always traversed)
 
     for (;;) {
         // ---- refill idle lanes (wave-aggregated dequeue) ----
@@ -214,7 +207,25 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
                         }
                         best_t = sph_t;  // closestIntersection.rayT = closestHit.rayT (:381)
                         best_tri = HG_NONE;
-                        mi = 0;
+                        // Exact mesh skip (see HgDevMesh::cull_*): a mesh whose root children the ray certainly
+                        // misses, or meets only beyond best_t, is not traversed; its 2 AABB tests are counted.
+                        // best_t only decreases afterwards, so the verdict stays valid for the whole ray.
+                        live = ~0ull;
+                        const float lim = best_t * 1.0001f + 1e-4f;
+                        const int ncull = kp.n_meshes < 64 ? kp.n_meshes : 64;
+                        for (int m = 0; m < ncull; ++m) {
+                            const HgDevMesh& md = kp.meshes[m];
+                            if (!md.cullable) continue;
+                            const float dA = ray_aabb(xyz(md.cull_a_lo), xyz(md.cull_a_hi), wo, winv);
+                            const float dB = ray_aabb(xyz(md.cull_b_lo), xyz(md.cull_b_hi), wo, winv);
+                            // a miss returns +INF (skip even when lim is INF); NaN never skips
+                            const bool farA = dA == HG_INF || dA > lim, farB = dB == HG_INF || dB > lim;
+                            if (farA && farB) {
+                                live &= ~(1ull << m);
+                                c_aabb += 2;
+                            }
+                        }
+                        mi = next_live(live, 0);
                         st = ST_MESH;
                     } else {
                         exhausted = true;
@@ -326,7 +337,7 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
             node = sp > 0 ? stk.pop(sp) : HG_NONE;
         }
         if (st == ST_TRAV && node == HG_NONE) {
-            mi++;
+            mi = next_live(live, mi + 1);
             st = ST_MESH;
         }
     }
