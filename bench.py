@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="mega", choices=["wavefront", "mega"])
+    ap.add_argument("--kernel", default="mega", choices=["wavefront", "mega", "regen"])
     ap.add_argument("--frames-per-step", type=int, default=1,
                     help="progressive frames per hg_render call per GPU-equivalent (semantics unchanged)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
@@ -121,7 +121,8 @@ def main():
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
 
     ctx = abi.Context(local_rank)
-    ctx.set_option(abi.HG_OPT_KERNEL, abi.HG_KERNEL_WAVEFRONT if args.kernel == "wavefront" else abi.HG_KERNEL_MEGA)
+    ctx.set_option(abi.HG_OPT_KERNEL, {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA,
+                                       "regen": abi.HG_KERNEL_MEGA_REGEN}[args.kernel])
     if args.timing:
         ctx.set_option(abi.HG_OPT_TIMING, 1)
     if args.refill:

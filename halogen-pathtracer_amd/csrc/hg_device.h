@@ -185,7 +185,6 @@ __device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, 
         const float4 cr = kp.spheres[3 * i];
         const float4 am = kp.spheres[3 * i + 1];
         const float4 b = kp.spheres[3 * i + 2];
-        c.spheres++;
         if (!(ray_aabb(xyz(am), xyz(b), ray.o, inv) < kp.far_)) continue;
         // sphere_intersection :266-303
         f3 center = xyz(cr);
@@ -267,7 +266,6 @@ __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     const uint64_t live = mesh_live_mask(kp, ray.o, winv, best_t, culled);
     c.aabb += 2 * culled;
-    c.meshes += uint32_t(kp.n_meshes);
     for (int mi = 0; mi < kp.n_meshes; ++mi) {
         bool active = mi >= 64 || ((live >> mi) & 1ull);
         if (!__any(active)) continue;  // the whole wave skips this mesh

@@ -20,6 +20,7 @@
 #include "hg_layout.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
                               const uint32_t* n_in, uint32_t* head, hipStream_t s);
@@ -670,9 +671,12 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (int rc = event_pair(c, ev)) return rc;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
-    const bool mega = c->kernel == HG_KERNEL_MEGA || p.halogenDebugMode != 0;
+    const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
-        hipError_t e = hg_launch_mega(kp, c->block == 128 ? 256 : c->block, c->counters_on != 0, c->stream);
+        const int mblock = c->block == 128 ? 256 : c->block;
+        hipError_t e = (c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0)
+                           ? hg_launch_mega_regen(kp, mblock, c->counters_on != 0, c->stream)
+                           : hg_launch_mega(kp, mblock, c->counters_on != 0, c->stream);
         if (e != hipSuccess) {
             c->free_events.push_back(ev);
             return fail(c, HG_E_HIP, "megakernel launch failed: %s", hipGetErrorString(e));
@@ -779,7 +783,7 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
     switch (option) {
         case HG_OPT_KERNEL:
-            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT)
+            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN)
                 return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
             c->kernel = value;
             return HG_OK;

@@ -160,8 +160,10 @@ enum {
 /* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v).  MEGA (default): one thread per pixel
  * for all frames of a dispatch, coherent 8x8-tile waves (always used for the debug views 1-5).  WAVEFRONT:
  * regenerating gen/trace/shade pipeline with compacted ray queues (kept as the A/B alternative; slower on this
- * workload because desynchronised lanes lose the tile coherence of the node fetches). */
-enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1 };
+ * workload because desynchronised lanes lose the tile coherence of the node fetches).
+ * MEGA_REGEN: the megakernel with per-lane path regeneration (a lane starts its next sample/frame as soon as
+ * its path ends instead of waiting for its wave). */
+enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64). */

@@ -15,7 +15,7 @@ GOLD = Path(__file__).resolve().parent / "golden"
 REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a diagnostic, the test is bitwise
 
 
-KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA}
+KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN}
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
