@@ -5,10 +5,11 @@
   python bench.py [--gpus N --steps K --warmup W] [--config C3]
   (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
-A STEP is one progressive frame (1 spp, the reference's unit of work: one HalogenCompute dispatch + one
-accumulation blit, RP:324-347) over the whole 1920x1080 image PER GPU: at N GPUs one step traces N frames of
-the image, its 8x8 tiles dealt round-robin to the N ranks, so per-GPU work is fixed ("scaling": "weak") and the
-accumulated image is bit-identical to a 1-GPU render of N*K frames.  The timed region (barrier + device sync
+A STEP is one complete C3 image PER GPU: 64 progressive frames of 1 spp (the reference's unit of work is one
+frame = one HalogenCompute dispatch + one accumulation blit, RP:324-347; C3 accumulates 64 of them) over the
+whole 1920x1080 image, issued as one hg_render(64) call.  At N GPUs one step traces N*64 frames of the image,
+its 8x8 tiles dealt round-robin to the N ranks, so per-GPU work is fixed ("scaling": "weak") and the
+accumulated image is bit-identical to a 1-GPU render of N*64*K frames.  The timed region (barrier + device sync
 on both sides, max over ranks) covers K steps and, for N > 1, the final RCCL gather of the tiles to rank 0.
 Scene build/upload and BVH build are outside it (as in the reference meter, HalogenDebugUI.cs:37-56).
 
@@ -38,6 +39,7 @@ from halogen import render_pass as rp  # noqa: E402
 from halogen import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+KERNEL_SYMBOL = {"regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
 METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
 
 
@@ -77,17 +79,17 @@ def cpu_baseline(packed, params, cube, width, height, seconds, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="mega", choices=["wavefront", "mega", "regen"])
-    ap.add_argument("--frames-per-step", type=int, default=1,
-                    help="progressive frames per hg_render call per GPU-equivalent (semantics unchanged)")
+    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen"])
+    ap.add_argument("--frames-per-step", type=int, default=64,
+                    help="progressive 1-spp frames per step per GPU-equivalent (64 = one C3 image)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
     ap.add_argument("--refill", type=int, default=0)
     ap.add_argument("--no-counters", action="store_true")
@@ -225,7 +227,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_launch_ms": mean_launch_s * 1e3,
-                         "kernel": "hg_trace_kernel"},
+                         "kernel": KERNEL_SYMBOL[args.kernel]},
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "setup_s": setup_s,

@@ -166,6 +166,13 @@ __device__ __forceinline__ float rcp_exact(float x) {
     return 1.0f / x;
 }
 
+// base + 32-bit byte offset: lets the compiler use the scalar-base + VGPR-offset load form (upload keeps every
+// scene array below 4 GiB, hg_runtime.hip)
+template <class T>
+__device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-259
     f3 t1 = (A - o) * inv;
     f3 t2 = (B - o) * inv;
@@ -178,8 +185,11 @@ __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-2
     return tMax > fmaxf(0.0f, tMin) ? tMin : HG_INF;
 }
 
-__device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c) {  // :357-376
-    float closest = h.t;
+// Returns the closest accepted sphere as index | (orientation < 0) << 31 (HG_NONE if none), its distance in t;
+// position/normal/material are resolved after the mesh pass (resolve_sphere), with the same arithmetic.
+__device__ uint32_t isect_spheres(const HgKernelParams& kp, const Ray& ray, float& t) {  // :357-376
+    float closest = t;
+    uint32_t best = HG_NONE;
     f3 inv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     for (int i = 0; i < kp.n_spheres; ++i) {
         const float4 cr = kp.spheres[3 * i];
@@ -194,20 +204,27 @@ __device__ void isect_spheres(const HgKernelParams& kp, const Ray& ray, Hit& h, 
         float disc = bq * bq - 4.0f * cq;
         if (!(disc >= 0.0f)) continue;  // rayT = INF: never accepted
         float hd = (-bq - __builtin_sqrtf(disc)) / 2.0f;
-        float orient = 1.0f;
+        uint32_t back = 0;
         if (hd < 0.0f) {
             hd = (-bq + __builtin_sqrtf(disc)) / 2.0f;
-            orient = -1.0f;
+            back = 0x80000000u;
         }
         if (hd < closest && hd > 0.0001f) {
-            h.t = hd;
-            h.orient = orient;
-            h.pos = ray.o + ray.d * hd;
-            h.n = normalize(h.pos - center) * orient;
-            h.mat = __float_as_uint(am.w);
             closest = hd;
+            best = uint32_t(i) | back;
         }
     }
+    t = closest;
+    return best;
+}
+__device__ __forceinline__ void resolve_sphere(const HgKernelParams& kp, const Ray& ray, uint32_t ref, Hit& h) {
+    const uint32_t i = ref & 0x7FFFFFFFu;
+    const float orient = (ref & 0x80000000u) ? -1.0f : 1.0f;
+    const float4 cr = kp.spheres[3 * i];
+    h.orient = orient;
+    h.pos = ray.o + ray.d * h.t;
+    h.n = normalize(h.pos - xyz(cr)) * orient;
+    h.mat = __float_as_uint(kp.spheres[3 * i + 1].w);
 }
 
 // Exact mesh skip (HgDevMesh::cull_*): bit m of the result is clear when the ray certainly misses both children of
@@ -251,12 +268,38 @@ __device__ __forceinline__ bool tri_accept(f3 lo, f3 ld, float4 a, float4 b, flo
            t > 0.0001f && t < best_t;
 }
 
-// get_ray_scene_intersection_mesh, :378-472.  `stack` points at this lane's column of the LDS stack.
+// Traversal stack: the first kLds entries of each lane live in LDS ([depth][lane], conflict-free), deeper entries
+// (rare: the BLAS depth cap is 32) spill to a per-lane global column, so the LDS footprint does not cap occupancy.
+// The LDS part is addressed through the address-space-3 array itself (a generic pointer here would turn every
+// access into a flat instruction).
+extern __shared__ uint32_t hg_lds_stack[];
+template <uint32_t kLds>
+struct Stack {
+    uint32_t lane;    // this lane's LDS column
+    uint32_t lds_stride;
+    uint32_t* spill;  // this lane's spill column
+    uint32_t spill_stride;
+    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
+        if (__builtin_expect(sp < kLds, 1)) hg_lds_stack[lane + sp * lds_stride] = v;
+        else spill[(sp - kLds) * spill_stride] = v;
+        ++sp;
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const {
+        --sp;
+        if (__builtin_expect(sp < kLds, 1)) return hg_lds_stack[lane + sp * lds_stride];
+        uint32_t v = spill[(sp - kLds) * spill_stride];
+        asm volatile("" : "+v"(v));  // keeps the two loads apart (merged, they become one flat load)
+        return v;
+    }
+};
+using MegaStack = Stack<HG_MEGA_LDS_STACK>;
+
+// get_ray_scene_intersection_mesh, :378-472.
 // The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
 // the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
 // while-while: all lanes descend inner nodes together until each holds a leaf, then test one leaf each.
-__device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, uint32_t* stack,
-                             uint32_t stride) {
+template <class Stk>
+__device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, const Stk& stk) {
     const float eps = 0.0001f;
     float best_t = h.t;  // closestIntersection.rayT starts at the sphere hit (:381)
     float best_u = 0.0f, best_v = 0.0f;
@@ -285,8 +328,9 @@ __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         while (__any(active)) {
             while (__any(active && !(node & HG_LEAF_BIT))) {
                 if (active && !(node & HG_LEAF_BIT)) {
-                    const float4* rec = kp.nodes + 4 * node;
-                    const float4 a_lo = rec[0], a_hi = rec[1], b_lo = rec[2], b_hi = rec[3];
+                    const uint32_t ro = node << 6;
+                    const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
+                                 b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
                     const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
                     const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
                     c.aabb += 2;
@@ -296,29 +340,36 @@ __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                     const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
                     const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
                     if (nearOk) {
-                        if (farOk) stack[(sp++) * stride] = farRef;
+                        if (farOk) stk.push(sp, farRef);
                         node = nearRef;
                     } else if (farOk) {
                         node = farRef;
                     } else {
-                        node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
+                        node = sp > 0 ? stk.pop(sp) : HG_NONE;
                     }
                 }
             }
             if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
-                const uint2 leaf = kp.leaves[node & ~HG_LEAF_BIT];
+                const uint2 leaf = ld_off(kp.leaves, (node & ~HG_LEAF_BIT) << 3);
                 uint32_t ti = leaf.x;
                 const uint32_t end = leaf.x + leaf.y;
-                float4 ta = kp.tri_a[ti], tb = kp.tri_b[ti];
-                float tc = kp.tri_c[ti];
+#if HG_TRI_PREFETCH
+                float4 ta = ld_off(kp.tri_a, ti << 4), tb = ld_off(kp.tri_b, ti << 4);
+                float tc = ld_off(kp.tri_c, ti << 2);
+#endif
                 for (; ti < end; ++ti) {
+#if HG_TRI_PREFETCH
                     const float4 a = ta, b = tb;
                     const float cz = tc;
                     if (ti + 1 < end) {
-                        ta = kp.tri_a[ti + 1];
-                        tb = kp.tri_b[ti + 1];
-                        tc = kp.tri_c[ti + 1];
+                        ta = ld_off(kp.tri_a, (ti + 1) << 4);
+                        tb = ld_off(kp.tri_b, (ti + 1) << 4);
+                        tc = ld_off(kp.tri_c, (ti + 1) << 2);
                     }
+#else
+                    const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+                    const float cz = ld_off(kp.tri_c, ti << 2);
+#endif
                     c.tri++;
                     float t, U, V;
                     bool front;
@@ -330,7 +381,7 @@ __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                         best_mesh = mi;
                     }
                 }
-                node = sp > 0 ? stack[(--sp) * stride] : HG_NONE;
+                node = sp > 0 ? stk.pop(sp) : HG_NONE;
             }
             if (node == HG_NONE) active = false;
         }
@@ -353,11 +404,13 @@ __device__ void isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                   ((n.x * m[8] + n.y * m[9]) + n.z * m[10]) + 0.0f * m[11]);
         h.n = normalize(w);
         h.pos = ray.o + ray.d * best_t;
+        return true;
     }
+    return false;
 }
 
-__device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ray, Counters& c, uint32_t* stack,
-                                         uint32_t stride) {  // get_ray_intersection :474-485
+template <class Stk>
+__device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ray, Counters& c, const Stk& stk) {  // get_ray_intersection :474-485
     Hit h;
     h.t = HG_INF;
     h.orient = 0.0f;
@@ -365,8 +418,8 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
     h.n = mk(0, 0, 0);
     h.mat = 0;
     c.rays++;
-    isect_spheres(kp, ray, h, c);
-    isect_meshes(kp, ray, h, c, stack, stride);
+    const uint32_t sph = isect_spheres(kp, ray, h.t);
+    if (!isect_meshes(kp, ray, h, c, stk) && sph != HG_NONE) resolve_sphere(kp, ray, sph, h);
     return h;
 }
 
@@ -551,8 +604,10 @@ __device__ f3 material_brdf(const HgKernelParams& kp, const Sampler& smp, Ray& r
 }
 
 // evaluate_material_hit :743-817
+// bt_out: the bounceTypes[] slot this hit increments (0 diffuse, 1 glossy, 2 transmission; a false hit counts as
+// transmission, :806)
 __device__ f3 evaluate_hit(const HgKernelParams& kp, const Sampler& smp, MediumStack& ms, Ray& ray, const Hit& hit,
-                           const Mat& mt, Bounces& bounce) {
+                           const Mat& mt, uint32_t& bt_out) {
     const Medium internal = medium_of(kp, hit.mat);
     const int32_t prio = __float_as_int(mt.prio_id_r2.x);
     Medium cur, hm;
@@ -581,12 +636,12 @@ __device__ f3 evaluate_hit(const HgKernelParams& kp, const Sampler& smp, MediumS
     if (trueHit) {
         uint32_t bt = 0;
         att = material_brdf(kp, smp, ray, hit, mt, cur, hm, bt);
-        bounce.bump(bt);
+        bt_out = bt;
         if (hit.orient > 0.0f && bt != 2u) medium_pop(kp, ms, internal.id);
     } else {
         ray.o = hit.pos - hit.n * 0.0001f;
         att = mk(1, 1, 1);
-        bounce.transmission++;
+        bt_out = 2u;
     }
     if (cur.id != 0xFFFFFFFFu) {
         att = mk(att.x * hg_expf(-cur.absorb.x * hit.t), att.y * hg_expf(-cur.absorb.y * hit.t),
@@ -596,20 +651,23 @@ __device__ f3 evaluate_hit(const HgKernelParams& kp, const Sampler& smp, MediumS
 }
 
 // trace_ray :876-950
+template <class Stk>
 __device__ f3 trace_ray(const HgKernelParams& kp, Sampler& smp, MediumStack& ms, Ray ray, Counters& c,
-                        uint32_t* stack, uint32_t stride) {
+                        const Stk& stk) {
     f3 acc = mk(0, 0, 0), thr = mk(1, 1, 1);
     float acc_rough = 0.0f;
     Bounces bounce{0, 0, 0};
     for (uint32_t it = 0; it <= kp.max_bounces; ++it) {
         if (bounce.diffuse > kp.max_diff || bounce.glossy > kp.max_glossy || bounce.transmission > kp.max_trans)
             break;
-        const Hit hit = intersect(kp, ray, c, stack, stride);
+        const Hit hit = intersect(kp, ray, c, stk);
         if (hit.t < kp.far_) {
             c.hits++;
             const Mat mt = load_mat(kp, hit.mat);
             acc = acc + xyz(mt.emis_rough) * thr;
-            const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bounce);
+            uint32_t bt = 0;
+            const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);
+            bounce.bump(bt);
             thr = thr * att;
             acc_rough += mt.emis_rough.w * thr.x;  // float3 -> float truncation (:911)
             const float rr = smp.get1(ID_RR);
@@ -626,26 +684,27 @@ __device__ f3 trace_ray(const HgKernelParams& kp, Sampler& smp, MediumStack& ms,
 }
 
 // trace_ray_debug :952-982
+template <class Stk>
 __device__ f3 trace_ray_debug(const HgKernelParams& kp, Sampler& smp, MediumStack& ms, Ray ray, Counters& c,
-                              uint32_t* stack, uint32_t stride) {
+                              const Stk& stk) {
     const uint32_t tri0 = c.tri, box0 = c.aabb;  // TriangleTests = AABBTests = 0
     switch (kp.debug_mode) {
         default:
             return mk(0, 0, 0);
         case 1: {
-            const Hit h = intersect(kp, ray, c, stack, stride);
+            const Hit h = intersect(kp, ray, c, stk);
             if (h.t < kp.far_) return xyz(kp.materials[5 * h.mat]);
             return sample_sky(kp, ray.d, kp.default_mip);
         }
         case 2: {
-            const Hit h = intersect(kp, ray, c, stack, stride);
+            const Hit h = intersect(kp, ray, c, stk);
             if (h.t < kp.far_) return mk((h.n.x + 1.0f) / 2.0f, (h.n.y + 1.0f) / 2.0f, (h.n.z + 1.0f) / 2.0f);
             return sample_sky(kp, ray.d, kp.default_mip);
         }
         case 3:
         case 4:
         case 5: {
-            trace_ray(kp, smp, ms, ray, c, stack, stride);
+            trace_ray(kp, smp, ms, ray, c, stk);
             const uint32_t tt = c.tri - tri0, bb = c.aabb - box0;
             if (kp.debug_mode == 3) {
                 if (tt > kp.tri_range) return mk(1, 1, 1);

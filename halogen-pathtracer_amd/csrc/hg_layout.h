@@ -29,6 +29,14 @@
 #define HG_TILE 8
 #define HG_MAX_CUBE_MIPS 16
 #define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
+#define HG_REGEN_MAX_BOUNCES 250  // regenerating megakernel: byte-packed bounce counters (larger: lockstep kernel)
+#define HG_REGEN_MAX_CHUNK 65535  // regenerating megakernel: frames per launch and spp limit (16-bit fields)
+#ifndef HG_TRI_PREFETCH
+#define HG_TRI_PREFETCH 1  // leaf loop: issue the next triangle's loads before testing the current one
+#endif
+#ifndef HG_MEGA_LDS_STACK
+#define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
+#endif
 
 struct alignas(16) HgDevMesh {
     float w2l[16];  // Unity column-major: column c = w2l[4c .. 4c+3]
@@ -63,8 +71,8 @@ struct HgKernelParams {
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
     uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
-    uint32_t* __restrict__ spill;  // wavefront trace: per-lane stack entries beyond HG_LDS_STACK (rarely touched)
-    uint32_t spill_stride;          // = threads of the persistent trace grid
+    uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)
+    uint32_t spill_stride;          // = threads of the launch grid
     // cubemap
     int32_t cube_size, cube_mips;
     uint32_t cube_mip_offset[HG_MAX_CUBE_MIPS];  // in float4 texels

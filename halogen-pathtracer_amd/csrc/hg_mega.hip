@@ -16,7 +16,6 @@ using namespace hgd;
 // allocation does not pay for trace_ray_debug.
 template <bool kCounters, bool kDebug>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
-    extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x & 63u;
     const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const int gtile = kp.rank + local_tile * kp.n_ranks;
@@ -26,8 +25,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKe
     Counters c{0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
     if (active) {
-        uint32_t* stack = lds_stack + threadIdx.x;
-        const uint32_t stride = blockDim.x;
+        const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x,
+                            kp.spill_stride};
         const size_t slot = size_t(local_tile) * 64 + lane;
         // HalogenCompute :1023-1033
         const float ndcx = (float(px) / kp.W) * 2.0f - 1.0f;
@@ -41,8 +40,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKe
             for (uint32_t s = 0; s < kp.spp; ++s) {
                 const Ray r = camera_ray(kp, smp, ndcx, ndcy);
                 paths++;
-                if (!kDebug) color = color + trace_ray(kp, smp, ms, r, c, stack, stride);
-                else color = color + trace_ray_debug(kp, smp, ms, r, c, stack, stride);
+                if (!kDebug) color = color + trace_ray(kp, smp, ms, r, c, stk);
+                else color = color + trace_ray_debug(kp, smp, ms, r, c, stk);
             }
             const float sppf = float(kp.spp);
             color = mk(color.x / sppf, color.y / sppf, color.z / sppf);
@@ -72,47 +71,55 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKe
     }
 }
 
+size_t hg_mega_lds_bytes(uint32_t stack_depth, int block) {
+    return size_t(stack_depth < HG_MEGA_LDS_STACK ? stack_depth : HG_MEGA_LDS_STACK) * size_t(block) *
+           sizeof(uint32_t);
+}
+
 // Regenerating variant (HG_KERNEL_MEGA_REGEN): each loop iteration runs ONE bounce (get_ray_intersection + one
-// body of trace_ray's loop) for every lane; a lane whose path ended starts its next sample / frame right away
-// (blending the finished frame into the accumulator), so lanes never wait for the longest path of their wave —
-// at the price of desynchronising the lanes' bounce depths (less coherent node fetches).
+// body of trace_ray's loop, :887-945) for every lane; a lane whose path ended starts its next sample / frame right
+// away (blending a finished frame into the accumulator), so lanes never idle until the longest path of their wave
+// ends — at the price of desynchronised bounce depths (less coherent node fetches).  Path state is packed to keep
+// the traversal's register budget: bounceTypes[3] + the bounce index in one word (host guarantees maxBounces <=
+// HG_REGEN_MAX_BOUNCES), frame + sample index in another (n_frames, spp < 2^16, host-chunked), the pixel's ndc /
+// accumulator slot recomputed at each regeneration.
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
-    extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x & 63u;
     const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
-    const int gtile = kp.rank + local_tile * kp.n_ranks;
-    const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-    const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-    bool work = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu && kp.n_frames > 0;
+    const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
+    bool work;
+    uint32_t px, py;
+    {
+        const int gtile = kp.rank + local_tile * kp.n_ranks;
+        px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+        py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+        work = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu && kp.n_frames > 0;
+    }
     Counters c{0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
-    uint32_t* stack = lds_stack + threadIdx.x;
-    const uint32_t stride = blockDim.x;
-    const size_t slot = size_t(local_tile) * 64 + lane;
-    const float ndcx = (float(px) / kp.W) * 2.0f - 1.0f;
-    const float ndcy = (float(py) / kp.H) * 2.0f - 1.0f;
-    const uint32_t pixel_id = pcg_hash(px + py * kp.Wu);
-    uint32_t f = 0, s = 0, iter = 0;
-    Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pixel_id, 0u};
+    uint32_t fs = 0;       // frame index << 16 | sample index
+    uint32_t bounce = 0;   // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
+    Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pcg_hash(px + py * kp.Wu), 0u};
     MediumStack ms{0ull, 0};
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
     f3 thr = mk(1, 1, 1), col = mk(0, 0, 0), sum = mk(0, 0, 0);
     float acc_rough = 0.0f;
-    Bounces bounce{0, 0, 0};
     if (work) {
-        ray = camera_ray(kp, smp, ndcx, ndcy);
+        ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
     }
     while (__any(work)) {
         if (work) {
-            const Hit hit = intersect(kp, ray, c, stack, stride);
+            const Hit hit = intersect(kp, ray, c, stk);
             bool alive = false;
             if (hit.t < kp.far_) {  // :898-936
                 c.hits++;
                 const Mat mt = load_mat(kp, hit.mat);
                 col = col + xyz(mt.emis_rough) * thr;
-                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bounce);
+                uint32_t bt = 0;
+                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);
+                bounce += 1u << (8u * bt);
                 thr = thr * att;
                 acc_rough += mt.emis_rough.w * thr.x;
                 const float rr = smp.get1(ID_RR);
@@ -120,22 +127,24 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
                 if (!(rr > contribution)) {
                     thr = thr * (1.0f / contribution);
-                    iter++;
-                    alive = iter <= kp.max_bounces && !(bounce.diffuse > kp.max_diff ||
-                                                       bounce.glossy > kp.max_glossy ||
-                                                       bounce.transmission > kp.max_trans);
+                    bounce += 1u << 24;
+                    alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
+                                                                 ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
+                                                                 ((bounce >> 16) & 0xFFu) > kp.max_trans);
                 }
             } else {  // :941
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
             if (!alive) {
                 sum = sum + col;  // RayColor += trace_ray(...)
-                ++s;
-                bool next = s < kp.spp;  // next sample: statics persist (:188-189)
+                ++fs;
+                bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    float4 acc = kp.acc[slot];
+                    const uint32_t lt = uint32_t(local_tile);
+                    float4* slot = kp.acc + (size_t(lt) * 64u + lane);
+                    float4 acc = *slot;
                     if (kp.accumulate) {
                         const float w = 1.0f / float(smp.frame);
                         const float k = 1.0f - w;
@@ -144,24 +153,25 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                     } else {
                         acc = make_float4(color.x, color.y, color.z, 1.0f);
                     }
-                    kp.acc[slot] = acc;
-                    ++f;
-                    if (f < uint32_t(kp.n_frames)) {  // next frame = next dispatch: statics reset
+                    *slot = acc;
+                    fs = (fs & 0xFFFF0000u) + 0x10000u;
+                    if ((fs >> 16) < uint32_t(kp.n_frames)) {  // next frame = next dispatch: statics reset
                         next = true;
-                        s = 0;
                         sum = mk(0, 0, 0);
-                        smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + f : 1u;
+                        smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
                         smp.offset = 0;
                         ms = MediumStack{0ull, 0};
                     }
                 }
                 if (next) {
-                    ray = camera_ray(kp, smp, ndcx, ndcy);
+                    const int gtile = kp.rank + local_tile * kp.n_ranks;
+                    const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+                    const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+                    ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     thr = mk(1, 1, 1);
                     col = mk(0, 0, 0);
                     acc_rough = 0.0f;
-                    bounce = Bounces{0, 0, 0};
-                    iter = 0;
+                    bounce = 0;
                     paths++;
                 } else {
                     work = false;
@@ -184,7 +194,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
     const int tiles_per_block = block / 64;
     const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
-    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block);
     if (counters)
         hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
     else
@@ -197,7 +207,7 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
     const int tiles_per_block = block / 64;
     const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
-    const size_t lds = size_t(kp.stack_depth) * size_t(block) * sizeof(uint32_t);
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block);
     const bool dbg = kp.debug_mode != 0;
     if (counters && dbg)
         hipLaunchKernelGGL((hg_trace_kernel<true, true>), dim3(grid), dim3(block), lds, stream, kp);

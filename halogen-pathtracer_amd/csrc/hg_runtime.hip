@@ -407,6 +407,10 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if ((n_spheres && !spheres) || (n_meshes && !meshes) || (n_materials && !materials) || (n_tris && !tris) ||
         (n_nodes && !blas))
         return fail(c, HG_E_INVALID, "null array with non-zero count");
+    // the traversal addresses nodes / triangles with 32-bit byte offsets (hg_device.h ld_off)
+    if (n_nodes >= (1 << 26) || n_tris >= (1 << 28))
+        return fail(c, HG_E_UNSUPPORTED, "scene too large: %d BLAS entries (max 2^26-1), %d triangles (max 2^28-1)",
+                    n_nodes, n_tris);
     if (n_materials > 255)
         return fail(c, HG_E_UNSUPPORTED, "at most 255 materials (medium stack packs material indices in bytes)");
     if (int rc = set_device(c)) return rc;
@@ -674,9 +678,29 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
         const int mblock = c->block == 128 ? 256 : c->block;
-        hipError_t e = (c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0)
-                           ? hg_launch_mega_regen(kp, mblock, c->counters_on != 0, c->stream)
-                           : hg_launch_mega(kp, mblock, c->counters_on != 0, c->stream);
+        const int mgrid = (c->n_local_tiles + mblock / 64 - 1) / (mblock / 64);
+        kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
+        if (kp.stack_depth > HG_MEGA_LDS_STACK) {  // stack entries beyond the LDS part: one column per thread
+            if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - HG_MEGA_LDS_STACK) * 4)) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+            kp.spill = static_cast<uint32_t*>(c->wf_spill.p);
+        }
+        const bool regen = c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0 &&
+                           kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
+        hipError_t e = hipSuccess;
+        if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
+            HgKernelParams kc = kp;
+            for (int done = 0; done < n_frames && e == hipSuccess;) {
+                kc.n_frames = std::min(n_frames - done, HG_REGEN_MAX_CHUNK);
+                kc.first_frame = accumulate ? kp.first_frame + done : 1;
+                e = hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                done += kc.n_frames;
+            }
+        } else {
+            e = hg_launch_mega(kp, mblock, c->counters_on != 0, c->stream);
+        }
         if (e != hipSuccess) {
             c->free_events.push_back(ev);
             return fail(c, HG_E_HIP, "megakernel launch failed: %s", hipGetErrorString(e));

@@ -115,24 +115,7 @@ __global__ __launch_bounds__(256) void hg_wf_gen(const HgKernelParams kp, uint32
 namespace {
 enum : uint32_t { ST_IDLE = 0, ST_MESH = 1, ST_TRAV = 2 };
 
-// Traversal stack: the first HG_LDS_STACK entries of each lane live in LDS ([depth][lane], conflict-free), deeper
-// entries (rare: the BLAS depth cap is 32) spill to a per-lane global array, so the LDS footprint stays small
-// enough for full occupancy.
-struct Stack {
-    uint32_t* lds;    // this lane's LDS column
-    uint32_t lds_stride;
-    uint32_t* spill;  // this lane's spill column
-    uint32_t spill_stride;
-    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
-        if (sp < HG_LDS_STACK) lds[sp * lds_stride] = v;
-        else spill[(sp - HG_LDS_STACK) * spill_stride] = v;
-        ++sp;
-    }
-    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const {
-        --sp;
-        return sp < HG_LDS_STACK ? lds[sp * lds_stride] : spill[(sp - HG_LDS_STACK) * spill_stride];
-    }
-};
+using WfStack = Stack<HG_LDS_STACK>;
 
 // first mesh index >= m that is not culled (meshes beyond 64 carry no cull bit and are always visited)
 __device__ __forceinline__ uint32_t next_live(uint64_t live, uint32_t m) {
@@ -146,9 +129,8 @@ __device__ __forceinline__ uint32_t next_live(uint64_t live, uint32_t m) {
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKernelParams kp, const uint32_t* __restrict__ q_in,
                                                    const uint32_t* __restrict__ n_in, uint32_t* __restrict__ head) {
-    extern __shared__ uint32_t lds_stack[];
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-    const Stack stk{lds_stack + threadIdx.x, blockDim.x, kp.spill + gtid, kp.spill_stride};
+    const WfStack stk{threadIdx.x, blockDim.x, kp.spill + gtid, kp.spill_stride};
     const uint32_t n = *n_in;
     const float eps = 0.0001f;
 
@@ -407,7 +389,9 @@ __global__ __launch_bounds__(256) void hg_wf_shade(const HgKernelParams kp, cons
                 }
                 const Mat mt = load_mat(kp, hit.mat);
                 col = col + xyz(mt.emis_rough) * thr;                       // :901-902
-                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bounce);  // :905
+                uint32_t bt = 0;
+                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);  // :905
+                bounce.bump(bt);
                 thr = thr * att;                                            // :908
                 acc_rough += mt.emis_rough.w * thr.x;                        // :911
                 const float rr = smp.get1(ID_RR);                           // :915

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name, extra rocprofv3 args...
   local name=$1; shift
-  timeout -k 10 420 rocprofv3 "$@" -d "$OUT/${TAG}_${name}" -o "$name" --output-format csv -- python3 bench.py $ARGS \
+  timeout -k 10 240 rocprofv3 "$@" -d "$OUT/${TAG}_${name}" -o "$name" --output-format csv -- python3 bench.py $ARGS \
       > "$OUT/${TAG}_${name}.log" 2>&1
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/${TAG}_${name}.log"; exit $rc; }
 }
