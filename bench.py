@@ -131,8 +131,7 @@ def main():
         ctx.set_option(abi.HG_OPT_REFILL, args.refill)
     if args.block:
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
-    if args.no_counters:
-        ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:
         ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
@@ -175,7 +174,23 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
 
+    timing = ctx.counters()  # kernel_ms / launches of the timed launches
+    replay_identical = None
+    timed_img = ctx.readback(W, H) if world == 1 and (not args.no_counters or args.save_image) else None
+    if not args.no_counters:
+        # Counting replay, untimed: the same K steps from the same cleared state with the device counters on give
+        # the exact traversal counts of the timed launches (the render is deterministic — checked on the image).
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+        ctx.reset_counters()
+        ctx.set_option(abi.HG_OPT_COUNTERS, 1)
+        for _ in range(args.steps):
+            ctx.render(frames_per_step, True)
+        ctx.synchronize()
+        if timed_img is not None:
+            replay_identical = bool(np.array_equal(timed_img.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
     cnt = ctx.counters()
+    cnt["kernel_ms"], cnt["launches"] = timing["kernel_ms"], timing["launches"]
     if dist is not None:
         import torch
 
@@ -230,13 +245,14 @@ def main():
                          "kernel": KERNEL_SYMBOL[args.kernel]},
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
+            "counting_replay_bit_identical": replay_identical,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},
             "cpu_baseline": None,
         }
         if args.save_image:
-            img = gathered.cpu().numpy() if gathered is not None else ctx.readback(W, H)
+            img = gathered.cpu().numpy() if gathered is not None else timed_img
             np.save(args.save_image, img)
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)

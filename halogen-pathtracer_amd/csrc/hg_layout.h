@@ -31,11 +31,17 @@
 #define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
 #define HG_REGEN_MAX_BOUNCES 250  // regenerating megakernel: byte-packed bounce counters (larger: lockstep kernel)
 #define HG_REGEN_MAX_CHUNK 65535  // regenerating megakernel: frames per launch and spp limit (16-bit fields)
+#ifndef HG_LOCK_WAVES
+#define HG_LOCK_WAVES 4  // lockstep megakernel (debug views, large-maxBounces fallback): waves/SIMD target
+#endif
+#ifndef HG_MEGA_WAVES
+#define HG_MEGA_WAVES 8  // regenerating megakernel: waves/SIMD target
+#endif
 #ifndef HG_TRI_PREFETCH
-#define HG_TRI_PREFETCH 1  // leaf loop: issue the next triangle's loads before testing the current one
+#define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
 #endif
 #ifndef HG_MEGA_LDS_STACK
-#define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
+#define HG_MEGA_LDS_STACK 10  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
 #endif
 
 struct alignas(16) HgDevMesh {

@@ -15,7 +15,7 @@ using namespace hgd;
 // kDebug: the debug views (HalogenDebugMode 1-5) get their own instantiation so the production kernel's register
 // allocation does not pay for trace_ray_debug.
 template <bool kCounters, bool kDebug>
-__global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
+__global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const int gtile = kp.rank + local_tile * kp.n_ranks;
@@ -83,11 +83,30 @@ size_t hg_mega_lds_bytes(uint32_t stack_depth, int block) {
 // the traversal's register budget: bounceTypes[3] + the bounce index in one word (host guarantees maxBounces <=
 // HG_REGEN_MAX_BOUNCES), frame + sample index in another (n_frames, spp < 2^16, host-chunked), the pixel's ndc /
 // accumulator slot recomputed at each regeneration.
+// A float3 of per-lane path state parked in LDS ([component][lane] after the traversal stack): the throughput,
+// radiance and sample sum are touched once per bounce, so they stay out of the registers the traversal needs.
+struct LaneVec {
+    uint32_t idx, stride;
+    __device__ __forceinline__ f3 get() const {
+        return mk(__uint_as_float(hg_lds_stack[idx]), __uint_as_float(hg_lds_stack[idx + stride]),
+                  __uint_as_float(hg_lds_stack[idx + 2 * stride]));
+    }
+    __device__ __forceinline__ void set(f3 v) const {
+        hg_lds_stack[idx] = __float_as_uint(v.x);
+        hg_lds_stack[idx + stride] = __float_as_uint(v.y);
+        hg_lds_stack[idx + 2 * stride] = __float_as_uint(v.z);
+    }
+};
+constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
+
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
+    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
+    const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
     bool work;
     uint32_t px, py;
     {
@@ -103,16 +122,19 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pcg_hash(px + py * kp.Wu), 0u};
     MediumStack ms{0ull, 0};
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
-    f3 thr = mk(1, 1, 1), col = mk(0, 0, 0), sum = mk(0, 0, 0);
     float acc_rough = 0.0f;
     if (work) {
         ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
+        s_thr.set(mk(1, 1, 1));
+        s_col.set(mk(0, 0, 0));
+        s_sum.set(mk(0, 0, 0));
     }
     while (__any(work)) {
         if (work) {
             const Hit hit = intersect(kp, ray, c, stk);
             bool alive = false;
+            f3 thr = s_thr.get(), col = s_col.get();
             if (hit.t < kp.far_) {  // :898-936
                 c.hits++;
                 const Mat mt = load_mat(kp, hit.mat);
@@ -136,16 +158,15 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
             if (!alive) {
-                sum = sum + col;  // RayColor += trace_ray(...)
+                f3 sum = s_sum.get() + col;  // RayColor += trace_ray(...)
                 ++fs;
                 bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    const uint32_t lt = uint32_t(local_tile);
-                    float4* slot = kp.acc + (size_t(lt) * 64u + lane);
+                    float4* slot = kp.acc + (size_t(uint32_t(local_tile)) * 64u + lane);
                     float4 acc = *slot;
-                    if (kp.accumulate) {
+                    if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
                         const float w = 1.0f / float(smp.frame);
                         const float k = 1.0f - w;
                         acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w, acc.z * k + color.z * w,
@@ -163,6 +184,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                         ms = MediumStack{0ull, 0};
                     }
                 }
+                s_sum.set(sum);
                 if (next) {
                     const int gtile = kp.rank + local_tile * kp.n_ranks;
                     const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
@@ -177,6 +199,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                     work = false;
                 }
             }
+            s_thr.set(thr);
+            s_col.set(col);
         }
     }
     if (kCounters) {
@@ -194,7 +218,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
     const int tiles_per_block = block / 64;
     const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
-    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block);
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
     if (counters)
         hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
     else
