@@ -217,7 +217,8 @@ def main():
         if tfile.exists():
             try:
                 t = json.loads(tfile.read_text())
-                if t.get("config") == args.config and t.get("width") == W and t.get("height") == H:
+                if (t.get("config") == args.config and t.get("width") == W and t.get("height") == H
+                        and t.get("frames_per_launch") == frames_per_step and t.get("kernel") == KERNEL_SYMBOL[args.kernel] + "<false>"):
                     traffic = t.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None

@@ -80,7 +80,7 @@ struct hg_ctx {
 
     // device / options
     int n_cu = 0;
-    int32_t kernel = HG_KERNEL_MEGA, block = 128, counters_on = 1, timing = 0, refill = 32;
+    int32_t kernel = HG_KERNEL_MEGA_REGEN, block = 128, counters_on = 1, timing = 0, refill = 32;
 };
 
 namespace {

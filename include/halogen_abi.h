@@ -157,12 +157,13 @@ enum {
     HG_E_UNSUPPORTED = -6
 };
 
-/* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v).  MEGA (default): one thread per pixel
- * for all frames of a dispatch, coherent 8x8-tile waves (always used for the debug views 1-5).  WAVEFRONT:
- * regenerating gen/trace/shade pipeline with compacted ray queues (kept as the A/B alternative; slower on this
- * workload because desynchronised lanes lose the tile coherence of the node fetches).
- * MEGA_REGEN: the megakernel with per-lane path regeneration (a lane starts its next sample/frame as soon as
- * its path ends instead of waiting for its wave). */
+/* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v); all produce bit-identical images.
+ * MEGA_REGEN (default): one lane per pixel of an 8x8-tile wave, one bounce per loop iteration; a lane whose path
+ *   ends starts its next sample / frame at once (per-lane path regeneration), so no lane idles until the
+ *   longest path of its wave ends.  Falls back to MEGA when maxBounces > 250 or samplesPerPixel >= 65535.
+ * MEGA: the lockstep form — each lane traces whole paths, frame after frame (also runs the debug views 1-5).
+ * WAVEFRONT: gen/trace/shade kernels over compacted ray queues (A/B alternative; slower on this workload, the
+ *   queue round trips cost more than the lane utilisation they recover). */
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).

@@ -148,3 +148,23 @@ def test_gpu_errors_are_loud(gpu):
             ctx.render(1)
         with pytest.raises(abi.HalogenError):
             ctx.set_tiling(3, 2)
+
+
+@pytest.mark.gpu
+def test_gpu_regen_limits_fall_back_bit_exact(gpu):
+    """maxBounces above the regenerating kernel's byte-packed limit (250) runs the lockstep megakernel: the image
+    and the work counters still equal the oracle's, and equal a lockstep render."""
+    import dataclasses
+    cfg = scenes.CONFIGS["C1"].resized(24, 16, 2)
+    settings = dataclasses.replace(scenes.settings_for(cfg), MaxBounces=300, DiffuseBounces=300, GlossyBounces=300)
+    s = rp.clamp_settings(settings)
+    packed = cases._scene("cornell", 10)
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), False)
+    assert params.maxBounces == 300
+    img, cnt = gpu_render(packed, params, 2, True, None, kernel="regen")
+    ref, ref_cnt = hg_oracle.render(packed, params, 2, True)
+    assert_bitwise(img, ref, "maxBounces 300")
+    lock, _ = gpu_render(packed, params, 2, True, None, kernel="mega")
+    assert_bitwise(img, lock, "regen fallback vs lockstep")
+    for k in ("rays", "tri_tests", "aabb_tests", "hits"):
+        assert cnt[k] == ref_cnt[k], (k, cnt[k], ref_cnt[k])

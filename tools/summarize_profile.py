@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Summarise one rocprofv3 profiling session of bench.py (tools/profile.sh TAG=...) into profiles/.
+
+  python tools/summarize_profile.py TAG [--frames-per-launch 64] [--config C3 --width 1920 --height 1080]
+
+Writes profiles/<TAG>_kernel_stats.csv (the --stats table as produced), profiles/<TAG>_summary.json (per-kernel
+average duration and PMC counters per launch) and, for the production kernel, profiles/pmc_traffic.json, read
+by bench.py as roofline.traffic.
+
+HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane loads (our node / triangle
+loads are global_load_dwordx4, 16 B per lane), so fetch bytes = FETCH_SIZE x 1024 x 2; WRITE_SIZE is exact for
+16-B-per-lane stores (the accumulator float4 stores).  The counters sit on the L2's fabric side, so Infinity
+Cache hits are included: the figure is an upper bound of DRAM traffic.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import shutil
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PROD = "hg_trace_regen_kernel<false>"
+
+
+def kname(raw: str) -> str:
+    return raw.replace("void ", "").split("(")[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--src", default=str(ROOT / "gpurun_out" / "prof"))
+    ap.add_argument("--frames-per-launch", type=int, default=64)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline")
+    a = ap.parse_args()
+    src = Path(a.src)
+    out = ROOT / "profiles"
+    out.mkdir(exist_ok=True)
+
+    stats_csv = src / f"{a.tag}_stats" / "stats_kernel_stats.csv"
+    shutil.copy(stats_csv, out / f"{a.tag}_kernel_stats.csv")
+    stats = {}
+    for r in csv.DictReader(open(stats_csv)):
+        stats[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                                   "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
+
+    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    calls = collections.defaultdict(lambda: collections.defaultdict(set))
+    for f in sorted(glob.glob(str(src / f"{a.tag}_*" / "*_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = kname(r["Kernel_Name"])
+            sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            calls[k][r["Counter_Name"]].add(r["Dispatch_Id"])
+    kernels = {}
+    for k in sorted(set(stats) | set(sums)):
+        pmc = {c: v / max(len(calls[k][c]), 1) for c, v in sums[k].items()}
+        d = {"stats": stats.get(k), "pmc_per_launch": pmc}
+        if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+            fetch = pmc["FETCH_SIZE"] * 1024 * 2
+            write = pmc["WRITE_SIZE"] * 1024
+            d["hbm_bytes_per_launch"] = fetch + write
+            d["fetch_bytes_per_launch"] = fetch
+            d["write_bytes_per_launch"] = write
+        if "TCC_HIT_sum" in pmc and "TCC_MISS_sum" in pmc:
+            d["l2_hit_rate"] = pmc["TCC_HIT_sum"] / max(pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"], 1)
+        if "SQ_WAVE_CYCLES" in pmc and pmc["SQ_WAVE_CYCLES"] > 0:
+            wc = pmc["SQ_WAVE_CYCLES"]
+            d["wave_cycle_split"] = {"wait_any": pmc.get("SQ_WAIT_ANY", 0) / wc,
+                                     "wait_inst_any": pmc.get("SQ_WAIT_INST_ANY", 0) / wc}
+        kernels[k] = d
+    summary = {"tag": a.tag, "command": f"rocprofv3 --kernel-trace --stats | --pmc <group> -- {a.command}",
+               "config": a.config, "width": a.width, "height": a.height,
+               "frames_per_launch": a.frames_per_launch, "kernels": kernels}
+    (out / f"{a.tag}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
+    if PROD in kernels and "hbm_bytes_per_launch" in kernels[PROD]:
+        t = {"tag": a.tag, "kernel": PROD, "config": a.config, "width": a.width, "height": a.height,
+             "frames_per_launch": a.frames_per_launch,
+             "hbm_bytes_per_launch": kernels[PROD]["hbm_bytes_per_launch"],
+             "note": "FETCH_SIZE*1024*2 + WRITE_SIZE*1024 per launch (MI355X_MICROARCH.md gfx950 corrections); "
+                     "fabric-side L2 counters, Infinity Cache hits included"}
+        (out / "pmc_traffic.json").write_text(json.dumps(t, indent=1) + "\n")
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
