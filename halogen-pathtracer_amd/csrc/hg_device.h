@@ -98,6 +98,19 @@ struct Sampler {
 constexpr uint32_t ID_FOCAL = 0, ID_JITTER = 1, ID_ROUGH = 2, ID_PROPERTY = 3, ID_RR = 4, BOUNCE_INC = 5;
 #define HLSL_PI (180.0f * HG_DEG2RAD)
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin to the 8 XCDs (b % 8), each with its own
+// L2.  Remapping b -> a contiguous range per XCD gives every XCD its own band of tiles, so the BVH nodes its
+// waves touch overlap more in its L2.  A bijection on [0, n) whatever the real placement (speed only).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+#if HG_XCD_REMAP
+    const uint32_t xcd = b & 7u, k = b >> 3, per = n >> 3, rem = n & 7u;
+    return xcd < rem ? xcd * (per + 1u) + k : rem * (per + 1u) + (xcd - rem) * per + k;
+#else
+    (void)n;
+    return b;
+#endif
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Per-lane path state
 // ---------------------------------------------------------------------------------------------------
@@ -294,6 +307,33 @@ struct Stack {
 };
 using MegaStack = Stack<HG_MEGA_LDS_STACK>;
 
+// first mesh index >= m whose cull bit is set (meshes >= 64 carry no bit and are always live); n if none
+__device__ __forceinline__ uint32_t next_live_mesh(uint64_t live, uint32_t m, uint32_t n) {
+    uint32_t r = 64u;
+    if (m < 64u) {
+        const uint64_t b = live & (~0ull << m);
+        if (b) r = uint32_t(__builtin_ctzll(b));
+    } else {
+        r = m;
+    }
+    return r < n ? r : n;
+}
+
+// world -> local ray of mesh m, direction NOT normalized (:390-392), its reciprocal and the root ref
+__device__ __forceinline__ void mesh_local_ray(const HgKernelParams& kp, const Ray& ray, uint32_t m, f3& lo, f3& ld,
+                                               f3& inv, uint32_t& root) {
+    const float4* md4 = reinterpret_cast<const float4*>(kp.meshes + m);
+    const float4 c0 = md4[0], c1 = md4[1], c2 = md4[2], c3 = md4[3];  // worldToLocal columns
+    root = __float_as_uint(md4[4].x);
+    lo = mk(((c0.x * ray.o.x + c1.x * ray.o.y) + c2.x * ray.o.z) + c3.x * 1.0f,
+            ((c0.y * ray.o.x + c1.y * ray.o.y) + c2.y * ray.o.z) + c3.y * 1.0f,
+            ((c0.z * ray.o.x + c1.z * ray.o.y) + c2.z * ray.o.z) + c3.z * 1.0f);
+    ld = mk(((c0.x * ray.d.x + c1.x * ray.d.y) + c2.x * ray.d.z) + c3.x * 0.0f,
+            ((c0.y * ray.d.x + c1.y * ray.d.y) + c2.y * ray.d.z) + c3.y * 0.0f,
+            ((c0.z * ray.d.x + c1.z * ray.d.y) + c2.z * ray.d.z) + c3.z * 0.0f);
+    inv = mk(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
+}
+
 // get_ray_scene_intersection_mesh, :378-472.
 // The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
 // the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
@@ -309,6 +349,81 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     const uint64_t live = mesh_live_mask(kp, ray.o, winv, best_t, culled);
     c.aabb += 2 * culled;
+#if HG_LANE_MESHES
+    // Per-lane mesh cursor: each lane walks its own live meshes in buffer order (the reference's order, so ties
+    // resolve identically) and moves to its next mesh as soon as it finishes one, so a wave waits for the lane
+    // with the most total work instead of the slowest lane of every mesh in turn.
+    const uint32_t nm = uint32_t(kp.n_meshes);
+    uint32_t mi = next_live_mesh(live, 0u, nm);
+    bool active = mi < nm;
+    f3 lo = mk(0, 0, 0), ld = mk(0, 0, 0), inv = mk(0, 0, 0);
+    uint32_t node = HG_NONE, sp = 0;
+    if (active) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
+    while (__any(active)) {
+        while (__any(active && !(node & HG_LEAF_BIT))) {
+            if (active && !(node & HG_LEAF_BIT)) {
+                const uint32_t ro = node << 6;
+                const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
+                             b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
+                const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
+                const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                c.aabb += 2;
+                const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                // reference (:430-444): push far, push near (each only if tEntry < closest), pop near
+                const bool bFirst = dB < dA;
+                const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
+                const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
+                if (nearOk) {
+                    if (farOk) stk.push(sp, farRef);
+                    node = nearRef;
+                } else if (farOk) {
+                    node = farRef;
+                } else {
+                    node = sp > 0 ? stk.pop(sp) : HG_NONE;
+                }
+            }
+        }
+        if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
+            const uint2 leaf = ld_off(kp.leaves, (node & ~HG_LEAF_BIT) << 3);
+            uint32_t ti = leaf.x;
+            const uint32_t end = leaf.x + leaf.y;
+#if HG_TRI_PREFETCH
+            float4 ta = ld_off(kp.tri_a, ti << 4), tb = ld_off(kp.tri_b, ti << 4);
+            float tc = ld_off(kp.tri_c, ti << 2);
+#endif
+            for (; ti < end; ++ti) {
+#if HG_TRI_PREFETCH
+                const float4 a = ta, b = tb;
+                const float cz = tc;
+                if (ti + 1 < end) {
+                    ta = ld_off(kp.tri_a, (ti + 1) << 4);
+                    tb = ld_off(kp.tri_b, (ti + 1) << 4);
+                    tc = ld_off(kp.tri_c, (ti + 1) << 2);
+                }
+#else
+                    const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+                    const float cz = ld_off(kp.tri_c, ti << 2);
+#endif
+                    c.tri++;
+                    float t, U, V;
+                    bool front;
+                    if (tri_accept(lo, ld, a, b, cz, best_t, t, U, V, front)) {
+                        best_t = t;
+                        best_u = U;
+                        best_v = V;
+                        best_tri = ti | (front ? 0u : 0x80000000u);
+                        best_mesh = int(mi);
+                    }
+                }
+                node = sp > 0 ? stk.pop(sp) : HG_NONE;
+            }
+            if (active && node == HG_NONE) {  // this mesh is done: the lane's next live mesh
+                mi = next_live_mesh(live, mi + 1u, nm);
+                if (mi < nm) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
+                else active = false;
+            }
+    }
+#else
     for (int mi = 0; mi < kp.n_meshes; ++mi) {
         bool active = mi >= 64 || ((live >> mi) & 1ull);
         if (!__any(active)) continue;  // the whole wave skips this mesh
@@ -386,6 +501,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             if (node == HG_NONE) active = false;
         }
     }
+#endif
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
         const HgDevMesh& md = kp.meshes[best_mesh];

@@ -37,6 +37,12 @@
 #ifndef HG_MEGA_WAVES
 #define HG_MEGA_WAVES 8  // regenerating megakernel: waves/SIMD target
 #endif
+#ifndef HG_LANE_MESHES
+#define HG_LANE_MESHES 1  // traversal: per-lane mesh cursor (1) or wave-uniform mesh loop (0)
+#endif
+#ifndef HG_XCD_REMAP
+#define HG_XCD_REMAP 0  // contiguous tile band per XCD: measured 24% SLOWER (static per-XCD imbalance), off
+#endif
 #ifndef HG_TRI_PREFETCH
 #define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
 #endif

@@ -17,7 +17,7 @@ using namespace hgd;
 template <bool kCounters, bool kDebug>
 __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const int gtile = kp.rank + local_tile * kp.n_ranks;
     const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
     const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
@@ -102,7 +102,7 @@ constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
     const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
     const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;

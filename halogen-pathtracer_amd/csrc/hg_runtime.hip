@@ -454,13 +454,10 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
         nrm[3 * t + 1] = f4(h.normalB.x - h.normalA.x, h.normalB.y - h.normalA.y, h.normalB.z - h.normalA.z, 0.0f);
         nrm[3 * t + 2] = f4(h.normalC.x - h.normalA.x, h.normalC.y - h.normalA.y, h.normalC.z - h.normalA.z, 0.0f);
     }
-    // ---- BLAS: validate every mesh's tree by DFS and build child-pair records + leaf table
-    std::vector<float4> rec(size_t(n_nodes) * 4, f4(0, 0, 0, 0));
-    std::vector<uint2> leaf(size_t(n_nodes), make_uint2(0, 0));
+    // ---- BLAS, pass 1: validate every mesh's tree by DFS (ranges, depth, sharing between meshes)
     std::vector<int64_t> owner(size_t(n_nodes), -1);  // (accOffset << 32 | triOffset) that produced the entry
     std::vector<HgDevMesh> dm(static_cast<size_t>(n_meshes));
     uint32_t max_depth = 0;
-    auto ref_of = [&](uint32_t g) { return g | (blas[g].triangleCount > 0 ? HG_LEAF_BIT : 0u); };
     std::vector<std::pair<uint32_t, uint32_t>> dfs;
     for (int mi = 0; mi < n_meshes; ++mi) {
         const HalogenMeshData& m = meshes[mi];
@@ -483,25 +480,65 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             if (e.triangleCount > 0) {
                 if (uint64_t(toff) + e.indexA + e.triangleCount > uint64_t(n_tris))
                     return fail(c, HG_E_INVALID, "mesh %d: leaf %u references triangles out of range", mi, g);
-                leaf[g] = make_uint2(toff + e.indexA, e.triangleCount);
             } else {
                 const uint64_t a = uint64_t(off) + e.indexA;
                 if (a + 1 >= uint64_t(n_nodes))
                     return fail(c, HG_E_INVALID, "mesh %d: node %u has children out of range", mi, g);
-                const BVHEntry& A = blas[a];
-                const BVHEntry& B = blas[a + 1];
-                rec[4 * size_t(g)] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z,
-                                       bits(ref_of(uint32_t(a))));
-                rec[4 * size_t(g) + 1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z,
-                                           bits(ref_of(uint32_t(a + 1))));
-                rec[4 * size_t(g) + 2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
-                rec[4 * size_t(g) + 3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
                 dfs.push_back({uint32_t(a + 1), depth + 1});
                 dfs.push_back({uint32_t(a), depth + 1});
             }
         }
+    }
+    // ---- BLAS, pass 2: device layout.  Inner nodes get a child-pair record (both children's boxes + refs, 64 B),
+    // leaves an entry of the leaf table.  Records are numbered in depth-first pre-order of sibling pairs: the two
+    // children of a node sit in one 128-B line (the far sibling, popped later, is usually still cached) and a
+    // subtree's records are contiguous.  Traversal follows refs only, so visit order and results are unchanged.
+    std::vector<uint32_t> dref(size_t(n_nodes), HG_NONE);  // device ref of each reference BVH entry
+    std::vector<float4> rec;
+    std::vector<uint2> leaf;
+    rec.reserve(size_t(n_nodes) * 4 + 8);
+    auto new_record = [&]() {
+        rec.resize(rec.size() + 4, f4(0, 0, 0, 0));
+        return uint32_t(rec.size() / 4 - 1);
+    };
+    std::vector<uint32_t> expand;
+    for (int mi = 0; mi < n_meshes; ++mi) {
+        const HalogenMeshData& m = meshes[mi];
+        const uint32_t off = m.accelerationBufferOffset, toff = m.triangleBufferOffset;
+        auto ref_for = [&](uint32_t g, bool with_sibling_pad) -> uint32_t {  // assigns a device ref on first use
+            if (dref[g] != HG_NONE) return dref[g];
+            const BVHEntry& e = blas[g];
+            if (e.triangleCount > 0) {
+                dref[g] = HG_LEAF_BIT | uint32_t(leaf.size());
+                leaf.push_back(make_uint2(toff + e.indexA, e.triangleCount));
+            } else {
+                if (with_sibling_pad && (rec.size() / 4) % 2 == 1) new_record();  // pair starts on an even record
+                dref[g] = new_record();
+                expand.push_back(g);
+            }
+            return dref[g];
+        };
+        const uint32_t root = ref_for(off, false);
+        while (!expand.empty()) {
+            const uint32_t g = expand.back();
+            expand.pop_back();
+            const uint32_t a = off + blas[g].indexA;
+            const bool both_new = dref[a] == HG_NONE && dref[a + 1] == HG_NONE && blas[a].triangleCount == 0 &&
+                                  blas[a + 1].triangleCount == 0;
+            const size_t mark = expand.size();
+            const uint32_t ra = ref_for(a, both_new);
+            const uint32_t rb = ref_for(a + 1, false);
+            if (expand.size() == mark + 2) std::swap(expand[mark], expand[mark + 1]);  // expand child A first
+            const BVHEntry& A = blas[a];
+            const BVHEntry& B = blas[a + 1];
+            const size_t r = 4 * size_t(dref[g]);
+            rec[r] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z, bits(ra));
+            rec[r + 1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z, bits(rb));
+            rec[r + 2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
+            rec[r + 3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
+        }
         std::memcpy(dm[mi].w2l, m.worldToLocal.m, sizeof dm[mi].w2l);
-        dm[mi].root_ref = ref_of(off);
+        dm[mi].root_ref = root;
         dm[mi].tri_offset = toff;
         dm[mi].material = m.materialIndex;
         dm[mi].cullable = 0;
@@ -511,6 +548,10 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             if (mesh_cull_boxes(m.worldToLocal, A, B, dm[mi])) dm[mi].cullable = 1;
         }
     }
+    if (rec.size() / 4 >= (size_t(1) << 26))
+        return fail(c, HG_E_UNSUPPORTED, "BLAS too large: %zu device node records", rec.size() / 4);
+    if (rec.empty()) new_record();
+    if (leaf.empty()) leaf.push_back(make_uint2(0, 0));
     c->stack_depth = std::max<uint32_t>(2u, (max_depth + 2 + 1) & ~1u);
 
     int rc;
@@ -677,7 +718,11 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
     const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
-        const int mblock = c->block == 128 ? 256 : c->block;
+        const bool regen = c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0 &&
+                           kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
+        // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
+        // tools/sweep12.txt), 256 for the lockstep one
+        const int mblock = c->block == 128 ? (regen ? 64 : 256) : c->block;
         const int mgrid = (c->n_local_tiles + mblock / 64 - 1) / (mblock / 64);
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
         if (kp.stack_depth > HG_MEGA_LDS_STACK) {  // stack entries beyond the LDS part: one column per thread
@@ -687,8 +732,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             }
             kp.spill = static_cast<uint32_t*>(c->wf_spill.p);
         }
-        const bool regen = c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0 &&
-                           kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
+
         hipError_t e = hipSuccess;
         if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
             HgKernelParams kc = kp;
