@@ -39,7 +39,7 @@ from halogen import render_pass as rp  # noqa: E402
 from halogen import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
-KERNEL_SYMBOL = {"regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
+KERNEL_SYMBOL = {"stream": "hg_trace_stream_kernel", "regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
 METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
 
 
@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen"])
+    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen", "stream"])
     ap.add_argument("--frames-per-step", type=int, default=64,
                     help="progressive 1-spp frames per step per GPU-equivalent (64 = one C3 image)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
@@ -124,7 +124,7 @@ def main():
 
     ctx = abi.Context(local_rank)
     ctx.set_option(abi.HG_OPT_KERNEL, {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA,
-                                       "regen": abi.HG_KERNEL_MEGA_REGEN}[args.kernel])
+                                       "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM}[args.kernel])
     if args.timing:
         ctx.set_option(abi.HG_OPT_TIMING, 1)
     if args.refill:

@@ -179,11 +179,20 @@ __device__ __forceinline__ float rcp_exact(float x) {
     return 1.0f / x;
 }
 
+// (first triangle, count) of a leaf ref (hg_layout.h): inline for small leaves, else from the leaf table
+__device__ __forceinline__ uint2 leaf_range(const HgKernelParams& kp, uint32_t ref);
+
 // base + 32-bit byte offset: lets the compiler use the scalar-base + VGPR-offset load form (upload keeps every
 // scene array below 4 GiB, hg_runtime.hip)
 template <class T>
 __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+__device__ __forceinline__ uint2 leaf_range(const HgKernelParams& kp, uint32_t ref) {
+    const uint32_t cnt = (ref >> HG_LEAF_CNT_SHIFT) & HG_LEAF_INLINE_MAX;
+    if (__builtin_expect(cnt != 0u, 1)) return make_uint2(ref & HG_LEAF_PAYLOAD, cnt);
+    return ld_off(kp.leaves, (ref & HG_LEAF_PAYLOAD) << 3);
 }
 
 __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-259
@@ -334,6 +343,27 @@ __device__ __forceinline__ void mesh_local_ray(const HgKernelParams& kp, const R
     inv = mk(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
 }
 
+// Accepted mesh hit (:452-471): interpolated normal x orientation through the inverse-transpose, hit position.
+__device__ __forceinline__ void resolve_mesh(const HgKernelParams& kp, const Ray& ray, float best_t, float best_u,
+                                             float best_v, uint32_t best_tri, uint32_t best_mesh, Hit& h) {
+    const HgDevMesh& md = kp.meshes[best_mesh];
+    const uint32_t tri = best_tri & 0x7FFFFFFFu;
+    const float orient = (best_tri & 0x80000000u) ? -1.0f : 1.0f;
+    h.t = best_t;
+    h.mat = md.material;
+    h.orient = orient;
+    const float4 n0 = kp.normals[3 * tri], d1 = kp.normals[3 * tri + 1], d2 = kp.normals[3 * tri + 2];
+    f3 n = (xyz(n0) + xyz(d1) * best_u) + xyz(d2) * best_v;
+    n = n * orient;
+    // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform)
+    const float* m = md.w2l;
+    f3 w = mk(((n.x * m[0] + n.y * m[1]) + n.z * m[2]) + 0.0f * m[3],
+              ((n.x * m[4] + n.y * m[5]) + n.z * m[6]) + 0.0f * m[7],
+              ((n.x * m[8] + n.y * m[9]) + n.z * m[10]) + 0.0f * m[11]);
+    h.n = normalize(w);
+    h.pos = ray.o + ray.d * best_t;
+}
+
 // get_ray_scene_intersection_mesh, :378-472.
 // The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
 // the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
@@ -384,7 +414,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             }
         }
         if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
-            const uint2 leaf = ld_off(kp.leaves, (node & ~HG_LEAF_BIT) << 3);
+            const uint2 leaf = leaf_range(kp, node);
             uint32_t ti = leaf.x;
             const uint32_t end = leaf.x + leaf.y;
 #if HG_TRI_PREFETCH
@@ -465,7 +495,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 }
             }
             if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
-                const uint2 leaf = ld_off(kp.leaves, (node & ~HG_LEAF_BIT) << 3);
+                const uint2 leaf = leaf_range(kp, node);
                 uint32_t ti = leaf.x;
                 const uint32_t end = leaf.x + leaf.y;
 #if HG_TRI_PREFETCH
@@ -504,22 +534,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
 #endif
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
-        const HgDevMesh& md = kp.meshes[best_mesh];
-        const uint32_t tri = best_tri & 0x7FFFFFFFu;
-        const float orient = (best_tri & 0x80000000u) ? -1.0f : 1.0f;
-        h.t = best_t;
-        h.mat = md.material;
-        h.orient = orient;
-        const float4 n0 = kp.normals[3 * tri], d1 = kp.normals[3 * tri + 1], d2 = kp.normals[3 * tri + 2];
-        f3 n = (xyz(n0) + xyz(d1) * best_u) + xyz(d2) * best_v;
-        n = n * orient;
-        // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform)
-        const float* m = md.w2l;
-        f3 w = mk(((n.x * m[0] + n.y * m[1]) + n.z * m[2]) + 0.0f * m[3],
-                  ((n.x * m[4] + n.y * m[5]) + n.z * m[6]) + 0.0f * m[7],
-                  ((n.x * m[8] + n.y * m[9]) + n.z * m[10]) + 0.0f * m[11]);
-        h.n = normalize(w);
-        h.pos = ray.o + ray.d * best_t;
+        resolve_mesh(kp, ray, best_t, best_u, best_v, best_tri, uint32_t(best_mesh), h);
         return true;
     }
     return false;
@@ -536,6 +551,107 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
     c.rays++;
     const uint32_t sph = isect_spheres(kp, ray, h.t);
     if (!isect_meshes(kp, ray, h, c, stk) && sph != HG_NONE) resolve_sphere(kp, ray, sph, h);
+    return h;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Resumable get_ray_intersection (:474-485) for the streaming kernel: the same spheres / exact mesh cull /
+// per-lane mesh cursor / while-while traversal as intersect(), with its state in a struct so a lane can stop
+// between steps (other lanes shade) and resume.  Same visit order, same counters, same result.
+// ---------------------------------------------------------------------------------------------------
+struct Trav {
+    f3 lo, ld, inv;        // ray in the current mesh's local space, 1/ld
+    float best_t, best_u, best_v, sph_t;
+    uint32_t best_tri;     // triangle | orientation<0 << 31, HG_NONE: no mesh hit yet
+    uint32_t best_mesh, sph, node, sp, mi;  // mi == n_meshes: traversal finished
+    uint64_t live;         // exact-cull mask of the meshes
+};
+
+__device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c) {
+    c.rays++;
+    t.sph_t = HG_INF;
+    t.sph = isect_spheres(kp, ray, t.sph_t);
+    t.best_t = t.sph_t;  // closestIntersection.rayT starts at the sphere hit (:381)
+    t.best_u = 0.0f;
+    t.best_v = 0.0f;
+    t.best_tri = HG_NONE;
+    t.best_mesh = 0;
+    uint32_t culled = 0;
+    const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
+    t.live = mesh_live_mask(kp, ray.o, winv, t.best_t, culled);
+    c.aabb += 2 * culled;
+    t.sp = 0;
+    t.node = HG_NONE;
+    const uint32_t nm = uint32_t(kp.n_meshes);
+    t.mi = next_live_mesh(t.live, 0u, nm);
+    if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, t.inv, t.node);
+}
+
+// One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
+// leaf, and move to the next live mesh when the current one is exhausted.
+template <class Stk>
+__device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
+                                          const Stk& stk, bool act) {
+    while (__any(act && !(t.node & HG_LEAF_BIT))) {
+        if (act && !(t.node & HG_LEAF_BIT)) {
+            const uint32_t ro = t.node << 6;
+            const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
+                         b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
+            const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), t.lo, t.inv);
+            const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), t.lo, t.inv);
+            c.aabb += 2;
+            const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+            const bool bFirst = dB < dA;  // :430-444
+            const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
+            const bool nearOk = (bFirst ? dB : dA) < t.best_t, farOk = (bFirst ? dA : dB) < t.best_t;
+            if (nearOk) {
+                if (farOk) stk.push(t.sp, farRef);
+                t.node = nearRef;
+            } else if (farOk) {
+                t.node = farRef;
+            } else {
+                t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+            }
+        }
+    }
+    if (act && t.node != HG_NONE) {  // :404-420
+        const uint2 leaf = leaf_range(kp, t.node);
+        const uint32_t end = leaf.x + leaf.y;
+        for (uint32_t ti = leaf.x; ti < end; ++ti) {
+            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+            const float cz = ld_off(kp.tri_c, ti << 2);
+            c.tri++;
+            float tt, U, V;
+            bool front;
+            if (tri_accept(t.lo, t.ld, a, b, cz, t.best_t, tt, U, V, front)) {
+                t.best_t = tt;
+                t.best_u = U;
+                t.best_v = V;
+                t.best_tri = ti | (front ? 0u : 0x80000000u);
+                t.best_mesh = t.mi;
+            }
+        }
+        t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+    }
+    if (act && t.node == HG_NONE) {
+        const uint32_t nm = uint32_t(kp.n_meshes);
+        t.mi = next_live_mesh(t.live, t.mi + 1u, nm);
+        if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, t.inv, t.node);
+    }
+}
+
+// The hit get_ray_intersection returns, from a finished traversal (:452-471 and the sphere pass).
+__device__ __forceinline__ Hit trav_hit(const HgKernelParams& kp, const Ray& ray, const Trav& t) {
+    Hit h;
+    h.t = t.sph_t;
+    h.orient = 0.0f;
+    h.pos = mk(0, 0, 0);
+    h.n = mk(0, 0, 0);
+    h.mat = 0;
+    if (t.best_t < (t.sph_t - 0.0001f) && t.best_t < kp.far_)
+        resolve_mesh(kp, ray, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, h);
+    else if (t.sph != HG_NONE)
+        resolve_sphere(kp, ray, t.sph, h);
     return h;
 }
 

@@ -26,6 +26,11 @@
 #include <stdint.h>
 
 #define HG_LEAF_BIT 0x80000000u
+// Leaf refs: HG_LEAF_BIT | count << HG_LEAF_CNT_SHIFT | first triangle, for leaves of 1..15 triangles starting
+// below 2^27 (no memory access to find a leaf's range); count field 0: the low bits index the leaf table instead.
+#define HG_LEAF_CNT_SHIFT 27
+#define HG_LEAF_INLINE_MAX 15u
+#define HG_LEAF_PAYLOAD ((1u << HG_LEAF_CNT_SHIFT) - 1u)
 #define HG_TILE 8
 #define HG_MAX_CUBE_MIPS 16
 #define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
@@ -36,6 +41,9 @@
 #endif
 #ifndef HG_MEGA_WAVES
 #define HG_MEGA_WAVES 8  // regenerating megakernel: waves/SIMD target
+#endif
+#ifndef HG_STREAM_TMIN
+#define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing
 #endif
 #ifndef HG_LANE_MESHES
 #define HG_LANE_MESHES 1  // traversal: per-lane mesh cursor (1) or wave-uniform mesh loop (0)

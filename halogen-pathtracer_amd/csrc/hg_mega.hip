@@ -226,6 +226,151 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
     return hipGetLastError();
 }
 
+// Streaming variant (HG_KERNEL_MEGA_STREAM): the regenerating kernel with a resumable traversal.  Lanes advance
+// their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
+// some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
+// their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
+template <bool kCounters>
+__global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
+    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
+    const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
+    const uint32_t nm = uint32_t(kp.n_meshes);
+    bool work;
+    uint32_t px, py;
+    {
+        const int gtile = kp.rank + local_tile * kp.n_ranks;
+        px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+        py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+        work = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu && kp.n_frames > 0;
+    }
+    Counters c{0, 0, 0, 0, 0, 0};
+    uint32_t paths = 0;
+    uint32_t fs = 0;       // frame index << 16 | sample index
+    uint32_t bounce = 0;   // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
+    Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pcg_hash(px + py * kp.Wu), 0u};
+    MediumStack ms{0ull, 0};
+    Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
+    float acc_rough = 0.0f;
+    Trav tv;
+    tv.mi = nm;
+    if (work) {
+        ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
+        paths++;
+        s_thr.set(mk(1, 1, 1));
+        s_col.set(mk(0, 0, 0));
+        s_sum.set(mk(0, 0, 0));
+        trav_begin(kp, ray, tv, c);
+    }
+    while (__any(work)) {
+        // ---- traversal rounds until few lanes are left traversing
+        for (;;) {
+            const bool act = work && tv.mi < nm;
+            const uint32_t n_act = uint32_t(__popcll(__ballot(act)));
+            if (n_act == 0) break;
+            if (n_act <= HG_STREAM_TMIN && __any(work && !act)) break;
+            trav_step(kp, ray, tv, c, stk, act);
+        }
+        // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
+        while (work && tv.mi >= nm) {
+            const Hit hit = trav_hit(kp, ray, tv);
+            bool alive = false;
+            f3 thr = s_thr.get(), col = s_col.get();
+            if (hit.t < kp.far_) {  // :898-936
+                c.hits++;
+                const Mat mt = load_mat(kp, hit.mat);
+                col = col + xyz(mt.emis_rough) * thr;
+                uint32_t bt = 0;
+                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);
+                bounce += 1u << (8u * bt);
+                thr = thr * att;
+                acc_rough += mt.emis_rough.w * thr.x;
+                const float rr = smp.get1(ID_RR);
+                smp.offset += BOUNCE_INC;
+                const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
+                if (!(rr > contribution)) {
+                    thr = thr * (1.0f / contribution);
+                    bounce += 1u << 24;
+                    alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
+                                                                 ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
+                                                                 ((bounce >> 16) & 0xFFu) > kp.max_trans);
+                }
+            } else {  // :941
+                col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
+            }
+            if (!alive) {
+                f3 sum = s_sum.get() + col;  // RayColor += trace_ray(...)
+                ++fs;
+                bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
+                if (!next) {
+                    const float sppf = float(kp.spp);
+                    const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
+                    float4* slot = kp.acc + (size_t(uint32_t(local_tile)) * 64u + lane);
+                    float4 acc = *slot;
+                    if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
+                        const float w = 1.0f / float(smp.frame);
+                        const float k = 1.0f - w;
+                        acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w, acc.z * k + color.z * w,
+                                          acc.w * k + 1.0f * w);
+                    } else {
+                        acc = make_float4(color.x, color.y, color.z, 1.0f);
+                    }
+                    *slot = acc;
+                    fs = (fs & 0xFFFF0000u) + 0x10000u;
+                    if ((fs >> 16) < uint32_t(kp.n_frames)) {  // next frame = next dispatch: statics reset
+                        next = true;
+                        sum = mk(0, 0, 0);
+                        smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
+                        smp.offset = 0;
+                        ms = MediumStack{0ull, 0};
+                    }
+                }
+                s_sum.set(sum);
+                if (next) {
+                    const int gtile = kp.rank + local_tile * kp.n_ranks;
+                    const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+                    const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+                    ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                    thr = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    acc_rough = 0.0f;
+                    bounce = 0;
+                    paths++;
+                    alive = true;
+                } else {
+                    work = false;
+                }
+            }
+            s_thr.set(thr);
+            s_col.set(col);
+            if (alive) trav_begin(kp, ray, tv, c);
+        }
+    }
+    if (kCounters) {
+        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits};
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const uint32_t sv = wave_sum(v[k]);
+            if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
+        }
+    }
+}
+
+hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
+    const int tiles_per_block = block / 64;
+    const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
+    if (grid == 0) return hipSuccess;
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
+    if (counters)
+        hipLaunchKernelGGL(hg_trace_stream_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
+    else
+        hipLaunchKernelGGL(hg_trace_stream_kernel<false>, dim3(grid), dim3(block), lds, stream, kp);
+    return hipGetLastError();
+}
+
 // Launcher used by the runtime (hg_runtime.hip)
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     const int tiles_per_block = block / 64;

@@ -21,6 +21,7 @@
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
                               const uint32_t* n_in, uint32_t* head, hipStream_t s);
@@ -509,8 +510,14 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             if (dref[g] != HG_NONE) return dref[g];
             const BVHEntry& e = blas[g];
             if (e.triangleCount > 0) {
-                dref[g] = HG_LEAF_BIT | uint32_t(leaf.size());
-                leaf.push_back(make_uint2(toff + e.indexA, e.triangleCount));
+                const uint64_t first = uint64_t(toff) + e.indexA;
+                if (e.triangleCount <= HG_LEAF_INLINE_MAX && first < HG_LEAF_PAYLOAD) {  // never encodes HG_NONE
+                    dref[g] = HG_LEAF_BIT | (e.triangleCount << HG_LEAF_CNT_SHIFT) | uint32_t(first);
+                } else {
+                    if (leaf.size() > HG_LEAF_PAYLOAD) return HG_NONE;  // reported below
+                    dref[g] = HG_LEAF_BIT | uint32_t(leaf.size());
+                    leaf.push_back(make_uint2(uint32_t(first), e.triangleCount));
+                }
             } else {
                 if (with_sibling_pad && (rec.size() / 4) % 2 == 1) new_record();  // pair starts on an even record
                 dref[g] = new_record();
@@ -519,6 +526,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             return dref[g];
         };
         const uint32_t root = ref_for(off, false);
+        if (root == HG_NONE) return fail(c, HG_E_UNSUPPORTED, "too many large BLAS leaves");
         while (!expand.empty()) {
             const uint32_t g = expand.back();
             expand.pop_back();
@@ -528,6 +536,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             const size_t mark = expand.size();
             const uint32_t ra = ref_for(a, both_new);
             const uint32_t rb = ref_for(a + 1, false);
+            if (ra == HG_NONE || rb == HG_NONE) return fail(c, HG_E_UNSUPPORTED, "too many large BLAS leaves");
             if (expand.size() == mark + 2) std::swap(expand[mark], expand[mark + 1]);  // expand child A first
             const BVHEntry& A = blas[a];
             const BVHEntry& B = blas[a + 1];
@@ -718,7 +727,8 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
     const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
-        const bool regen = c->kernel == HG_KERNEL_MEGA_REGEN && p.halogenDebugMode == 0 &&
+        const bool regen = (c->kernel == HG_KERNEL_MEGA_REGEN || c->kernel == HG_KERNEL_MEGA_STREAM) &&
+                           p.halogenDebugMode == 0 &&
                            kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweep12.txt), 256 for the lockstep one
@@ -739,7 +749,9 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, HG_REGEN_MAX_CHUNK);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
-                e = hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                e = c->kernel == HG_KERNEL_MEGA_STREAM
+                        ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
+                        : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
                 done += kc.n_frames;
             }
         } else {
@@ -851,7 +863,8 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
     switch (option) {
         case HG_OPT_KERNEL:
-            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN)
+            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
+                value != HG_KERNEL_MEGA_STREAM)
                 return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
             c->kernel = value;
             return HG_OK;

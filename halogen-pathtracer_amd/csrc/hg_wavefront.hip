@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
 
         // ---- one leaf per lane: triangles tested branch-free, the next one's loads issued ahead ----
         if (st == ST_TRAV && node != HG_NONE) {
-            const uint2 leaf = kp.leaves[node & ~HG_LEAF_BIT];
+            const uint2 leaf = leaf_range(kp, node);
             uint32_t ti = leaf.x;
             const uint32_t end = leaf.x + leaf.y;
             float4 ta = kp.tri_a[ti], tb = kp.tri_b[ti];

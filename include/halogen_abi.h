@@ -164,7 +164,9 @@ enum {
  * MEGA: the lockstep form — each lane traces whole paths, frame after frame (also runs the debug views 1-5).
  * WAVEFRONT: gen/trace/shade kernels over compacted ray queues (A/B alternative; slower on this workload, the
  *   queue round trips cost more than the lane utilisation they recover). */
-enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2 };
+/* MEGA_STREAM: MEGA_REGEN with a resumable traversal — lanes that finished traversing shade and start their next
+ *   ray while the stragglers keep traversing (same limits and fallback as MEGA_REGEN). */
+enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64). */

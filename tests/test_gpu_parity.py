@@ -15,7 +15,8 @@ GOLD = Path(__file__).resolve().parent / "golden"
 REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a diagnostic, the test is bitwise
 
 
-KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN}
+KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN,
+           "stream": abi.HG_KERNEL_MEGA_STREAM}
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
