@@ -94,10 +94,15 @@ def main():
     ap.add_argument("--refill", type=int, default=0)
     ap.add_argument("--no-counters", action="store_true")
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
+                         "reports that rank's own Mpaths/s, not a contract line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    emu = args.emulate_ranks if world == 1 and args.emulate_ranks > 1 else 0
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
@@ -131,16 +136,18 @@ def main():
         ctx.set_option(abi.HG_OPT_REFILL, args.refill)
     if args.block:
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
+    if args.frame_split >= 0:
+        ctx.set_option(abi.HG_OPT_FRAME_SPLIT, args.frame_split)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:
         ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
     ctx.resize(W, H)
-    ctx.set_tiling(rank, world)
+    ctx.set_tiling(rank, emu or world)
     ctx.set_params(params)
     setup_s = time.perf_counter() - t_setup
 
-    frames_per_step = world * args.frames_per_step  # per-GPU work fixed: frame-equivalents of the image per GPU
+    frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
     for _ in range(args.warmup):
         ctx.render(frames_per_step, True)
     ctx.synchronize()
@@ -205,6 +212,8 @@ def main():
         totals = cnt
 
     total_paths = W * H * frames_per_step * args.steps
+    if emu:  # this GPU traced only its 1/N share of the tiles
+        total_paths = ctx.local_tile_count() * 64 * frames_per_step * args.steps
     result = None
     if rank == 0:
         launches = max(cnt["launches"], 1)
@@ -247,6 +256,7 @@ def main():
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "counting_replay_bit_identical": replay_identical,
+            "emulated_ranks": emu or None,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},

@@ -87,6 +87,11 @@ struct HgKernelParams {
     int32_t use_cube;
     int32_t n_spheres, n_meshes;
     int32_t first_frame, n_frames, accumulate;
+    // frame-parallel split (regenerating kernel): frame_split waves share each tile, wave k tracing frames
+    // [k*n_frames/split, (k+1)*n_frames/split) into frame_color[frame][slot]; hg_blend_frames then applies the
+    // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
+    int32_t frame_split;
+    float4* __restrict__ frame_color;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane

@@ -102,7 +102,13 @@ constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
+    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
+    const int local_tile = int(gw % nlt);
+    const uint32_t chunk = gw / nlt;
+    const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
+    const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
     const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
     const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
@@ -113,13 +119,13 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         const int gtile = kp.rank + local_tile * kp.n_ranks;
         px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
         py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-        work = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu && kp.n_frames > 0;
+        work = chunk < split && px < kp.Wu && py < kp.Hu && f_end > f_begin;
     }
     Counters c{0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
-    uint32_t fs = 0;       // frame index << 16 | sample index
-    uint32_t bounce = 0;   // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
-    Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pcg_hash(px + py * kp.Wu), 0u};
+    uint32_t fs = f_begin << 16;  // frame index << 16 | sample index
+    uint32_t bounce = 0;          // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
+    Sampler smp{kp.accumulate ? uint32_t(kp.first_frame) + f_begin : 1u, pcg_hash(px + py * kp.Wu), 0u};
     MediumStack ms{0ull, 0};
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
     float acc_rough = 0.0f;
@@ -164,19 +170,25 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    float4* slot = kp.acc + (size_t(uint32_t(local_tile)) * 64u + lane);
-                    float4 acc = *slot;
-                    if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                        const float w = 1.0f / float(smp.frame);
-                        const float k = 1.0f - w;
-                        acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w, acc.z * k + color.z * w,
-                                          acc.w * k + 1.0f * w);
+                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + lane;
+                    if (split > 1u) {  // frame-parallel: this frame's colour, blended later in frame order
+                        kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
+                            make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
-                        acc = make_float4(color.x, color.y, color.z, 1.0f);
+                        float4* slot = kp.acc + slot_i;
+                        float4 acc = *slot;
+                        if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
+                            const float w = 1.0f / float(smp.frame);
+                            const float k = 1.0f - w;
+                            acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w,
+                                              acc.z * k + color.z * w, acc.w * k + 1.0f * w);
+                        } else {
+                            acc = make_float4(color.x, color.y, color.z, 1.0f);
+                        }
+                        *slot = acc;
                     }
-                    *slot = acc;
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    if ((fs >> 16) < uint32_t(kp.n_frames)) {  // next frame = next dispatch: statics reset
+                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
@@ -214,9 +226,38 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     }
 }
 
+// Frame-parallel epilogue: acc = acc*(1-w) + c_f*w for f in frame order (AccumulationShader.shader:33), exactly
+// the per-frame blend the kernel does itself when frame_split == 1.
+__global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc, const float4* __restrict__ colors,
+                                                       uint32_t n_slots, int32_t n_frames, int32_t first_frame,
+                                                       int32_t accumulate) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    float4 a = acc[i];
+    for (int32_t f = 0; f < n_frames; ++f) {
+        const float4 c = colors[size_t(f) * n_slots + i];
+        if (accumulate) {
+            const float w = 1.0f / float(uint32_t(first_frame + f));
+            const float k = 1.0f - w;
+            a = make_float4(a.x * k + c.x * w, a.y * k + c.y * w, a.z * k + c.z * w, a.w * k + 1.0f * w);
+        } else {
+            a = make_float4(c.x, c.y, c.z, 1.0f);
+        }
+    }
+    acc[i] = a;
+}
+
+hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) {
+    const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
+    if (n_slots == 0) return hipSuccess;
+    hipLaunchKernelGGL(hg_blend_frames, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc, kp.frame_color,
+                       n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+    return hipGetLastError();
+}
+
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     const int tiles_per_block = block / 64;
-    const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
+    const int grid = (kp.n_local_tiles * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
     if (counters)

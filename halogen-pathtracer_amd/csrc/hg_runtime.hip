@@ -22,6 +22,7 @@
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
 hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
                               const uint32_t* n_in, uint32_t* head, hipStream_t s);
@@ -33,6 +34,7 @@ int64_t hg_wf_selftest_rcp(int64_t* tested);
 
 namespace {
 
+constexpr size_t kFrameColorCap = size_t(4) << 30;  // frame-parallel colour buffer cap (bytes)
 constexpr uint32_t kMaxStack = 64;  // LDS stack entries per lane; BLAS depth must be <= kMaxStack - 2
 
 struct DevBuf {
@@ -70,6 +72,7 @@ struct hg_ctx {
     DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
     DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
     DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
+    DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -82,6 +85,7 @@ struct hg_ctx {
     // device / options
     int n_cu = 0;
     int32_t kernel = HG_KERNEL_MEGA_REGEN, block = 128, counters_on = 1, timing = 0, refill = 32;
+    int32_t frame_split = 0;  // 0: automatic (see hg_render)
 };
 
 namespace {
@@ -386,7 +390,7 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -687,6 +691,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.first_frame = accumulate ? p.frameCount : 1;
     kp.n_frames = n_frames;
     kp.accumulate = accumulate ? 1 : 0;
+    kp.frame_split = 1;
     kp.tiles_x = c->tiles_x;
     kp.rank = c->rank;
     kp.n_ranks = c->n_ranks;
@@ -733,7 +738,29 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweep12.txt), 256 for the lockstep one
         const int mblock = c->block == 128 ? (regen ? 64 : 256) : c->block;
-        const int mgrid = (c->n_local_tiles + mblock / 64 - 1) / (mblock / 64);
+        // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
+        // about 16x as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
+        // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
+        // (bit-identical).  Measured (tools/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
+        // rank's share at N=8 314 -> 1212.
+        const bool stream_k = c->kernel == HG_KERNEL_MEGA_STREAM;
+        const int64_t tiles = c->n_local_tiles;
+        const int64_t resident = int64_t(c->n_cu) * 4 * HG_MEGA_WAVES;  // wave slots of the regen kernel
+        int split = 1;
+        if (regen && !stream_k && n_frames > 1 && tiles > 0) {
+            if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
+            else split = int(std::min<int64_t>(n_frames, (16 * resident + tiles - 1) / tiles));
+        }
+        int chunk_max = HG_REGEN_MAX_CHUNK;
+        if (split > 1) {
+            const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
+            chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
+            if (int rc = ensure(c, c->frame_color, per_frame * size_t(std::min(n_frames, chunk_max)))) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+        }
+        const int mgrid = int((tiles * split + mblock / 64 - 1) / (mblock / 64));
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
         if (kp.stack_depth > HG_MEGA_LDS_STACK) {  // stack entries beyond the LDS part: one column per thread
             if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - HG_MEGA_LDS_STACK) * 4)) {
@@ -746,12 +773,14 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         hipError_t e = hipSuccess;
         if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
             HgKernelParams kc = kp;
+            kc.frame_color = static_cast<float4*>(c->frame_color.p);
             for (int done = 0; done < n_frames && e == hipSuccess;) {
-                kc.n_frames = std::min(n_frames - done, HG_REGEN_MAX_CHUNK);
+                kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
-                e = c->kernel == HG_KERNEL_MEGA_STREAM
-                        ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
-                        : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                kc.frame_split = std::min(split, kc.n_frames);
+                e = stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
+                             : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                if (e == hipSuccess && kc.frame_split > 1) e = hg_launch_blend_frames(kc, c->stream);
                 done += kc.n_frames;
             }
         } else {
@@ -881,6 +910,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_REFILL:
             if (value < 1 || value > 64) return fail(c, HG_E_INVALID, "refill must be 1..64");
             c->refill = value;
+            return HG_OK;
+        case HG_OPT_FRAME_SPLIT:
+            if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");
+            c->frame_split = value;
             return HG_OK;
         default:
             return fail(c, HG_E_INVALID, "unknown option %d", option);

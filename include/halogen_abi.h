@@ -169,8 +169,12 @@ enum {
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
- * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64). */
-enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5 };
+ * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).
+ * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then
+ *   blended in frame order, bit-identical): 0 = automatic (about 16 launches' worth of the GPU's wave slots per
+ *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile. */
+enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
+       HG_OPT_FRAME_SPLIT = 6 };
 
 int hg_abi_version(void);
 

@@ -169,3 +169,26 @@ def test_gpu_regen_limits_fall_back_bit_exact(gpu):
     assert_bitwise(img, lock, "regen fallback vs lockstep")
     for k in ("rays", "tri_tests", "aabb_tests", "hits"):
         assert cnt[k] == ref_cnt[k], (k, cnt[k], ref_cnt[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [1, 3, 7])
+def test_gpu_frame_parallel_split_bit_exact(gpu, split):
+    """Frame-parallel split (several waves per tile on disjoint frame ranges, colours blended in frame order) gives
+    the image and counters of the unsplit render; also with a first FrameCount > 1 and without accumulation."""
+    for name, first in (("c1_64", 1), ("c1_64", 5), ("c1_48_noacc", 1), ("glass_64x36", 1)):
+        packed, params, cube, frames, acc = cases.setup(name, first_frame=first)
+        frames = 8
+        refs = []
+        for sp in (1, split):
+            with abi.Context(0) as ctx:
+                ctx.set_option(abi.HG_OPT_FRAME_SPLIT, sp)
+                refs.append(gpu_render(packed, params, frames, acc, cube, ctx=ctx, kernel="regen"))
+        assert_bitwise(refs[1][0], refs[0][0], f"{name} first={first} split {split}")
+        for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+            assert refs[1][1][k] == refs[0][1][k], (k, refs[1][1][k], refs[0][1][k])
+    ref, _ = hg_oracle.render(*cases.setup("c1_64")[:2], 8, True)
+    with abi.Context(0) as ctx:
+        ctx.set_option(abi.HG_OPT_FRAME_SPLIT, split)
+        img, _ = gpu_render(*cases.setup("c1_64")[:2], 8, True, None, ctx=ctx, kernel="regen")
+    assert_bitwise(img, ref, f"split {split} vs oracle")
