@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--refill", type=int, default=0)
     ap.add_argument("--no-counters", action="store_true")
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
@@ -104,6 +106,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     emu = args.emulate_ranks if world == 1 and args.emulate_ranks > 1 else 0
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = int(os.environ.get("HALOGEN_BENCH_DEVICE", local_rank))  # rehearsal: every rank on one GPU
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
@@ -113,8 +116,12 @@ def main():
         import torch.distributed as dist_mod
 
         dist = dist_mod
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = f"cuda:{device}" if args.dist_backend == "nccl" else "cpu"
 
     cfg = scenes.CONFIGS[args.config]
     if args.width and args.height:
@@ -127,7 +134,7 @@ def main():
     W, H = cfg.width, cfg.height
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
 
-    ctx = abi.Context(local_rank)
+    ctx = abi.Context(device)
     ctx.set_option(abi.HG_OPT_KERNEL, {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA,
                                        "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM}[args.kernel])
     if args.timing:
@@ -175,9 +182,9 @@ def main():
         from halogen import distributed as hd
 
         n_local = ctx.local_tile_count()
-        local = torch.empty((n_local, 64, 4), dtype=torch.float32, device=f"cuda:{local_rank}")
+        local = torch.empty((n_local, 64, 4), dtype=torch.float32, device=f"cuda:{device}")
         ctx.copy_tiles_device(local.data_ptr(), local.numel() * 4)
-        gathered = hd.gather_tiles(local, rank, world, W, H)
+        gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H)
     barrier()
     dt = time.perf_counter() - t0
 
@@ -201,11 +208,11 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         keys = ["paths", "rays", "tri_tests", "aabb_tests", "mesh_visits", "sphere_tests", "hits"]
-        v = torch.tensor([float(cnt[k]) for k in keys], dtype=torch.float64, device=f"cuda:{local_rank}")
+        v = torch.tensor([float(cnt[k]) for k in keys], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(v)
         totals = dict(zip(keys, (int(x) for x in v.tolist())))
     else:

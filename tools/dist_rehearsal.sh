@@ -1,0 +1,23 @@
+#!/bin/bash
+# Rehearsal of bench.py's N-rank path on ONE GPU: 2 (or 3) ranks over gloo, every rank on device 0.  The gathered
+# image of N ranks x F frames must equal the 1-rank image of N*F frames (weak scaling semantics), bit for bit.
+set -u
+mkdir -p gpurun_out/dist
+export HALOGEN_BENCH_DEVICE=0
+ARGS="--config C3 --width 640 --height 360 --steps 1 --warmup 1 --no-cpu-baseline --frames-per-step 8"
+for n in 2 3; do
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+      --master-port $((29500 + n)) bench.py --gpus $n --dist-backend gloo $ARGS \
+      --save-image gpurun_out/dist/img_n$n.npy > gpurun_out/dist/bench_n$n.json 2> gpurun_out/dist/bench_n$n.err
+  rc=$?; echo "n=$n rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dist/bench_n$n.err; exit $rc; }
+  cat gpurun_out/dist/bench_n$n.json
+  timeout -k 10 300 python bench.py $ARGS --frames-per-step $((8 * n)) --save-image gpurun_out/dist/img_1x$n.npy \
+      > gpurun_out/dist/bench_1x$n.json 2> gpurun_out/dist/bench_1x$n.err
+  rc=$?; echo "1-rank reference rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dist/bench_1x$n.err; exit $rc; }
+  python -c "
+import numpy as np, sys
+a = np.load('gpurun_out/dist/img_n$n.npy'); b = np.load('gpurun_out/dist/img_1x$n.npy')
+same = a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+print('n=$n gathered image bit-identical to 1-rank render:', same, a.shape)
+sys.exit(0 if same else 1)" || exit 1
+done
