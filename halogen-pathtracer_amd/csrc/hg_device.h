@@ -302,13 +302,13 @@ struct Stack {
     uint32_t* spill;  // this lane's spill column
     uint32_t spill_stride;
     __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
-        if (__builtin_expect(sp < kLds, 1)) hg_lds_stack[lane + sp * lds_stride] = v;
+        if (__builtin_expect(sp < kLds, 1)) hg_lds_stack[__umul24(sp, lds_stride) + lane] = v;  // full-rate mad24
         else spill[(sp - kLds) * spill_stride] = v;
         ++sp;
     }
     __device__ __forceinline__ uint32_t pop(uint32_t& sp) const {
         --sp;
-        if (__builtin_expect(sp < kLds, 1)) return hg_lds_stack[lane + sp * lds_stride];
+        if (__builtin_expect(sp < kLds, 1)) return hg_lds_stack[__umul24(sp, lds_stride) + lane];
         uint32_t v = spill[(sp - kLds) * spill_stride];
         asm volatile("" : "+v"(v));  // keeps the two loads apart (merged, they become one flat load)
         return v;
@@ -390,8 +390,12 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     uint32_t node = HG_NONE, sp = 0;
     if (active) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
     while (__any(active)) {
-        while (__any(active && !(node & HG_LEAF_BIT))) {
+#if HG_TRAV_IFIF
+        if (active && !(node & HG_LEAF_BIT)) {  // if-if: one node step per round, leaves tested in the same round
+#else
+        while (__any(active && !(node & HG_LEAF_BIT))) {  // while-while: descend until every lane is at a leaf
             if (active && !(node & HG_LEAF_BIT)) {
+#endif
                 const uint32_t ro = node << 6;
                 const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
                              b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
@@ -411,8 +415,12 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 } else {
                     node = sp > 0 ? stk.pop(sp) : HG_NONE;
                 }
+#if HG_TRAV_IFIF
+        } else
+#else
             }
         }
+#endif
         if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
             const uint2 leaf = leaf_range(kp, node);
             uint32_t ti = leaf.x;

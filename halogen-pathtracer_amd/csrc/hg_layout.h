@@ -40,10 +40,13 @@
 #define HG_LOCK_WAVES 4  // lockstep megakernel (debug views, large-maxBounces fallback): waves/SIMD target
 #endif
 #ifndef HG_MEGA_WAVES
-#define HG_MEGA_WAVES 8  // regenerating megakernel: waves/SIMD target
+#define HG_MEGA_WAVES 6  // regenerating megakernel: waves/SIMD target
 #endif
 #ifndef HG_STREAM_TMIN
 #define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing
+#endif
+#ifndef HG_TRAV_IFIF
+#define HG_TRAV_IFIF 0  // traversal rounds: 1 = if-if (node step or leaf per round), 0 = while-while
 #endif
 #ifndef HG_LANE_MESHES
 #define HG_LANE_MESHES 1  // traversal: per-lane mesh cursor (1) or wave-uniform mesh loop (0)
@@ -55,7 +58,7 @@
 #define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
 #endif
 #ifndef HG_MEGA_LDS_STACK
-#define HG_MEGA_LDS_STACK 10  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
+#define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
 #endif
 
 struct alignas(16) HgDevMesh {
