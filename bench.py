@@ -263,6 +263,8 @@ def main():
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "counting_replay_bit_identical": replay_identical,
+            "simd_utilisation": {"descent": cnt["aabb_tests"] / 2 / max(64 * cnt["node_rounds"], 1),
+                                 "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1)} if counters_ok else None,
             "emulated_ranks": emu or None,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],

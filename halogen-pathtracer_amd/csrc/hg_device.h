@@ -31,7 +31,13 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 __device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ float rcp_exact(float x);
+// normalize = v * (1/sqrt(dot(v,v))) (hg_fmath.h hg_rnorm) with the correctly rounded reciprocal (same bits)
+#if HG_RCP_NORMALIZE
+__device__ __forceinline__ f3 normalize(f3 a) { return a * rcp_exact(__builtin_sqrtf(dot(a, a))); }
+#else
 __device__ __forceinline__ f3 normalize(f3 a) { return a * hg_rnorm(dot(a, a)); }
+#endif
 __device__ __forceinline__ f3 lerp(f3 a, f3 b, float s) { return a + (b - a) * s; }
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 
@@ -115,8 +121,12 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 // Per-lane path state
 // ---------------------------------------------------------------------------------------------------
 struct Counters {
-    uint32_t rays, tri, aabb, meshes, spheres, hits;
+    uint32_t rays, tri, aabb, node_rounds, tri_rounds, hits;  // *_rounds: wave-level loop iterations (one lane counts)
 };
+// 1 in exactly one active lane (the lowest): summed over lanes, counts the wave-level executions of a code point
+__device__ __forceinline__ uint32_t wave_once() {
+    return __lane_id() == uint32_t(__builtin_ctzll(__ballot(1))) ? 1u : 0u;
+}
 
 // bounceTypes[3] of trace_ray (:887) kept as three named registers (a runtime-indexed array would go to
 // scratch memory on gfx950)
@@ -394,6 +404,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         if (active && !(node & HG_LEAF_BIT)) {  // if-if: one node step per round, leaves tested in the same round
 #else
         while (__any(active && !(node & HG_LEAF_BIT))) {  // while-while: descend until every lane is at a leaf
+            c.node_rounds += wave_once();
             if (active && !(node & HG_LEAF_BIT)) {
 #endif
                 const uint32_t ro = node << 6;
@@ -407,6 +418,12 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 const bool bFirst = dB < dA;
                 const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
                 const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
+                // near (far pushed if it is also entered), else far, else pop — decided branch-free
+#if HG_BRANCHLESS_DESCENT
+                if (nearOk && farOk) stk.push(sp, farRef);
+                node = nearOk ? nearRef : farRef;
+                if (!nearOk && !farOk) node = sp > 0 ? stk.pop(sp) : HG_NONE;
+#else
                 if (nearOk) {
                     if (farOk) stk.push(sp, farRef);
                     node = nearRef;
@@ -415,6 +432,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 } else {
                     node = sp > 0 ? stk.pop(sp) : HG_NONE;
                 }
+#endif
 #if HG_TRAV_IFIF
         } else
 #else
@@ -430,6 +448,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             float tc = ld_off(kp.tri_c, ti << 2);
 #endif
             for (; ti < end; ++ti) {
+                c.tri_rounds += wave_once();
 #if HG_TRI_PREFETCH
                 const float4 a = ta, b = tb;
                 const float cz = tc;
@@ -601,6 +620,7 @@ template <class Stk>
 __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
                                           const Stk& stk, bool act) {
     while (__any(act && !(t.node & HG_LEAF_BIT))) {
+        c.node_rounds += wave_once();
         if (act && !(t.node & HG_LEAF_BIT)) {
             const uint32_t ro = t.node << 6;
             const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
@@ -612,20 +632,16 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             const bool bFirst = dB < dA;  // :430-444
             const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
             const bool nearOk = (bFirst ? dB : dA) < t.best_t, farOk = (bFirst ? dA : dB) < t.best_t;
-            if (nearOk) {
-                if (farOk) stk.push(t.sp, farRef);
-                t.node = nearRef;
-            } else if (farOk) {
-                t.node = farRef;
-            } else {
-                t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
-            }
+            if (nearOk && farOk) stk.push(t.sp, farRef);
+            t.node = nearOk ? nearRef : farRef;
+            if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
         }
     }
     if (act && t.node != HG_NONE) {  // :404-420
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
         for (uint32_t ti = leaf.x; ti < end; ++ti) {
+            c.tri_rounds += wave_once();
             const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
             const float cz = ld_off(kp.tri_c, ti << 2);
             c.tri++;
@@ -914,7 +930,7 @@ __device__ f3 trace_ray(const HgKernelParams& kp, Sampler& smp, MediumStack& ms,
             smp.offset += BOUNCE_INC;
             const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
             if (rr > contribution) break;
-            thr = thr * (1.0f / contribution);
+            thr = thr * rcp_exact(contribution);
         } else {
             acc = acc + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             break;

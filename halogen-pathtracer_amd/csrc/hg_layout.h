@@ -45,6 +45,12 @@
 #ifndef HG_STREAM_TMIN
 #define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing
 #endif
+#ifndef HG_RCP_NORMALIZE
+#define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)
+#endif
+#ifndef HG_BRANCHLESS_DESCENT
+#define HG_BRANCHLESS_DESCENT 0  // descent: select-based near/far/pop decision
+#endif
 #ifndef HG_TRAV_IFIF
 #define HG_TRAV_IFIF 0  // traversal rounds: 1 = if-if (node step or leaf per round), 0 = while-while
 #endif

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKe
             color = mk(color.x / sppf, color.y / sppf, color.z / sppf);
             float4 acc = kp.acc[slot];  // read-modify-write per frame: 32 B, keeps 4 VGPRs free while tracing
             if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                const float w = 1.0f / float(fc);
+                const float w = rcp_exact(float(fc));
                 const float k = 1.0f - w;
                 acc.x = acc.x * k + color.x * w;
                 acc.y = acc.y * k + color.y * w;
@@ -61,10 +61,10 @@ __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKe
     }
     if (kCounters) {
         // every ray transforms into every mesh and prefilters every sphere: those counts follow from c.rays
-        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
-                               c.rays * uint32_t(kp.n_spheres), c.hits};
+        const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
+                               c.rays * uint32_t(kp.n_spheres), c.hits, c.node_rounds, c.tri_rounds};
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
+        for (int k = 0; k < 9; ++k) {
             const uint32_t s = wave_sum(v[k]);
             if (lane == 0 && s) atomicAdd(kp.counters + k, (unsigned long long)s);
         }
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 smp.offset += BOUNCE_INC;
                 const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
                 if (!(rr > contribution)) {
-                    thr = thr * (1.0f / contribution);
+                    thr = thr * rcp_exact(contribution);
                     bounce += 1u << 24;
                     alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
                                                                  ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                         float4* slot = kp.acc + slot_i;
                         float4 acc = *slot;
                         if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                            const float w = 1.0f / float(smp.frame);
+                            const float w = rcp_exact(float(smp.frame));
                             const float k = 1.0f - w;
                             acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w,
                                               acc.z * k + color.z * w, acc.w * k + 1.0f * w);
@@ -216,10 +216,10 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         }
     }
     if (kCounters) {
-        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
-                               c.rays * uint32_t(kp.n_spheres), c.hits};
+        const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
+                               c.rays * uint32_t(kp.n_spheres), c.hits, c.node_rounds, c.tri_rounds};
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
+        for (int k = 0; k < 9; ++k) {
             const uint32_t sv = wave_sum(v[k]);
             if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
         }
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc,
     for (int32_t f = 0; f < n_frames; ++f) {
         const float4 c = colors[size_t(f) * n_slots + i];
         if (accumulate) {
-            const float w = 1.0f / float(uint32_t(first_frame + f));
+            const float w = rcp_exact(float(uint32_t(first_frame + f)));
             const float k = 1.0f - w;
             a = make_float4(a.x * k + c.x * w, a.y * k + c.y * w, a.z * k + c.z * w, a.w * k + 1.0f * w);
         } else {
@@ -274,7 +274,13 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
+    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
+    const int local_tile = int(gw % nlt);
+    const uint32_t chunk = gw / nlt;
+    const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
+    const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
     const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
     const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
@@ -286,13 +292,13 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(con
         const int gtile = kp.rank + local_tile * kp.n_ranks;
         px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
         py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-        work = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu && kp.n_frames > 0;
+        work = chunk < split && px < kp.Wu && py < kp.Hu && f_end > f_begin;
     }
     Counters c{0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
-    uint32_t fs = 0;       // frame index << 16 | sample index
-    uint32_t bounce = 0;   // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
-    Sampler smp{uint32_t(kp.accumulate ? kp.first_frame : 1), pcg_hash(px + py * kp.Wu), 0u};
+    uint32_t fs = f_begin << 16;  // frame index << 16 | sample index
+    uint32_t bounce = 0;          // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
+    Sampler smp{kp.accumulate ? uint32_t(kp.first_frame) + f_begin : 1u, pcg_hash(px + py * kp.Wu), 0u};
     MediumStack ms{0ull, 0};
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
     float acc_rough = 0.0f;
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(con
                 smp.offset += BOUNCE_INC;
                 const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
                 if (!(rr > contribution)) {
-                    thr = thr * (1.0f / contribution);
+                    thr = thr * rcp_exact(contribution);
                     bounce += 1u << 24;
                     alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
                                                                  ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
@@ -349,19 +355,25 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(con
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    float4* slot = kp.acc + (size_t(uint32_t(local_tile)) * 64u + lane);
-                    float4 acc = *slot;
-                    if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                        const float w = 1.0f / float(smp.frame);
-                        const float k = 1.0f - w;
-                        acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w, acc.z * k + color.z * w,
-                                          acc.w * k + 1.0f * w);
+                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + lane;
+                    if (split > 1u) {  // frame-parallel: this frame's colour, blended later in frame order
+                        kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
+                            make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
-                        acc = make_float4(color.x, color.y, color.z, 1.0f);
+                        float4* slot = kp.acc + slot_i;
+                        float4 acc = *slot;
+                        if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
+                            const float w = rcp_exact(float(smp.frame));
+                            const float k = 1.0f - w;
+                            acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w,
+                                              acc.z * k + color.z * w, acc.w * k + 1.0f * w);
+                        } else {
+                            acc = make_float4(color.x, color.y, color.z, 1.0f);
+                        }
+                        *slot = acc;
                     }
-                    *slot = acc;
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    if ((fs >> 16) < uint32_t(kp.n_frames)) {  // next frame = next dispatch: statics reset
+                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
@@ -391,9 +403,10 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(con
         }
     }
     if (kCounters) {
-        const uint32_t v[7] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits};
+        const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
+                               c.node_rounds, c.tri_rounds};
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
+        for (int k = 0; k < 9; ++k) {
             const uint32_t sv = wave_sum(v[k]);
             if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
         }
@@ -402,7 +415,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(con
 
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     const int tiles_per_block = block / 64;
-    const int grid = (kp.n_local_tiles + tiles_per_block - 1) / tiles_per_block;
+    const int grid = (kp.n_local_tiles * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
     if (counters)

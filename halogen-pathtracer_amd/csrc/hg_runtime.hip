@@ -747,7 +747,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         const int64_t tiles = c->n_local_tiles;
         const int64_t resident = int64_t(c->n_cu) * 4 * HG_MEGA_WAVES;  // wave slots of the regen kernel
         int split = 1;
-        if (regen && !stream_k && n_frames > 1 && tiles > 0) {
+        if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
             else split = int(std::min<int64_t>(n_frames, (16 * resident + tiles - 1) / tiles));
         }
@@ -866,6 +866,8 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->mesh_visits = v[4];
     out->sphere_tests = v[5];
     out->hits = v[6];
+    out->node_rounds = v[7];
+    out->tri_rounds = v[8];
     return HG_OK;
 }
 

@@ -78,7 +78,8 @@ class HgCounters(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
-                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64)]
+                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
+                ("tri_rounds", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

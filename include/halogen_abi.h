@@ -143,6 +143,9 @@ typedef struct hg_counters {
     uint64_t launches;     /* hg_render dispatches timed in kernel_ms */
     double trace_ms;       /* summed device time of the traversal kernel alone (only with HG_OPT_TIMING on) */
     uint64_t trace_launches; /* traversal kernel launches timed in trace_ms */
+    uint64_t node_rounds;  /* megakernels: wave-level iterations of the BVH descent loop (SIMD utilisation of the
+                              descent = aabb_tests / 2 / (64 * node_rounds)) */
+    uint64_t tri_rounds;   /* megakernels: wave-level iterations of the leaf loop (tri_tests / (64 * tri_rounds)) */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;

@@ -1,0 +1,5 @@
+set -u
+for c in C3 C2 C5; do
+  timeout -k 10 300 python bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/util_$c.json 2> gpurun_out/util_$c.err || exit $?
+  python3 -c "import json; r=json.load(open('gpurun_out/util_$c.json')); print('$c', round(r['value']), r['simd_utilisation'], r['counters_per_path'])"
+done
