@@ -39,7 +39,7 @@ from halogen import render_pass as rp  # noqa: E402
 from halogen import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
-KERNEL_SYMBOL = {"stream": "hg_trace_stream_kernel", "regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
+KERNEL_SYMBOL = {"pool": "hg_trace_pool_kernel", "stream": "hg_trace_stream_kernel", "regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
 METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
 
 
@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen", "stream"])
+    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
                     help="progressive 1-spp frames per step per GPU-equivalent (64 = one C3 image)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
+    ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
                          "reports that rank's own Mpaths/s, not a contract line")
@@ -136,7 +137,8 @@ def main():
 
     ctx = abi.Context(device)
     ctx.set_option(abi.HG_OPT_KERNEL, {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA,
-                                       "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM}[args.kernel])
+                                       "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
+                                       "pool": abi.HG_KERNEL_MEGA_POOL}[args.kernel])
     if args.timing:
         ctx.set_option(abi.HG_OPT_TIMING, 1)
     if args.refill:
@@ -145,6 +147,8 @@ def main():
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
     if args.frame_split >= 0:
         ctx.set_option(abi.HG_OPT_FRAME_SPLIT, args.frame_split)
+    if args.descent_t >= -1:
+        ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:

@@ -403,7 +403,14 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
 #if HG_TRAV_IFIF
         if (active && !(node & HG_LEAF_BIT)) {  // if-if: one node step per round, leaves tested in the same round
 #else
-        while (__any(active && !(node & HG_LEAF_BIT))) {  // while-while: descend until every lane is at a leaf
+        // while-while, relaxed: descend while more than kp.descent_t lanes are still descending (0: until every
+        // lane is at a leaf), and in any case until at least one lane can make other progress (a leaf to test or
+        // its mesh finished); the few stragglers pause while the others test their leaves.  Each lane's own
+        // sequence of node / leaf steps is unchanged.
+        for (;;) {
+            const uint32_t n_desc = uint32_t(__popcll(__ballot(active && !(node & HG_LEAF_BIT))));
+            if (n_desc == 0u) break;
+            if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(active)))) break;
             c.node_rounds += wave_once();
             if (active && !(node & HG_LEAF_BIT)) {
 #endif
@@ -439,7 +446,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             }
         }
 #endif
-        if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
+        if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order
             const uint2 leaf = leaf_range(kp, node);
             uint32_t ti = leaf.x;
             const uint32_t end = leaf.x + leaf.y;
@@ -521,7 +528,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                     }
                 }
             }
-            if (active && node != HG_NONE) {  // a leaf: its triangles in order, next one's loads issued ahead
+            if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order
                 const uint2 leaf = leaf_range(kp, node);
                 uint32_t ti = leaf.x;
                 const uint32_t end = leaf.x + leaf.y;

@@ -36,6 +36,12 @@
 #define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
 #define HG_REGEN_MAX_BOUNCES 250  // regenerating megakernel: byte-packed bounce counters (larger: lockstep kernel)
 #define HG_REGEN_MAX_CHUNK 65535  // regenerating megakernel: frames per launch and spp limit (16-bit fields)
+#ifndef HG_POOL_TILES
+#define HG_POOL_TILES 4  // path-pool kernel: 8x8 tiles (64 paths each) per wave
+#endif
+#ifndef HG_POOL_WAVES
+#define HG_POOL_WAVES 6  // path-pool kernel: waves/SIMD target
+#endif
 #ifndef HG_LOCK_WAVES
 #define HG_LOCK_WAVES 4  // lockstep megakernel (debug views, large-maxBounces fallback): waves/SIMD target
 #endif
@@ -50,6 +56,12 @@
 #endif
 #ifndef HG_BRANCHLESS_DESCENT
 #define HG_BRANCHLESS_DESCENT 0  // descent: select-based near/far/pop decision
+#endif
+#ifndef HG_DESCENT_T
+#define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
+#endif
+#ifndef HG_DESCENT_DEEP
+#define HG_DESCENT_DEEP 16
 #endif
 #ifndef HG_TRAV_IFIF
 #define HG_TRAV_IFIF 0  // traversal rounds: 1 = if-if (node step or leaf per round), 0 = while-while
@@ -101,9 +113,11 @@ struct HgKernelParams {
     // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
     int32_t frame_split;
     float4* __restrict__ frame_color;
+    float4* __restrict__ pool;  // path-pool kernel: per-wave path slots (hg_pool.hip)
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
+    uint32_t descent_t;    // relaxed while-while threshold (hg_device.h isect_meshes), 0 = classic while-while
     uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
     uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)
     uint32_t spill_stride;          // = threads of the launch grid

@@ -23,6 +23,9 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
+hipError_t hg_launch_mega_pool(const HgKernelParams& kp, bool counters, hipStream_t stream);
+uint32_t hg_pool_slots();
+uint32_t hg_pool_tiles();
 hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
                               const uint32_t* n_in, uint32_t* head, hipStream_t s);
@@ -73,6 +76,7 @@ struct hg_ctx {
     DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
     DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
     DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
+    DevBuf pool;                 // path-pool kernel: per-wave path slots
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -86,6 +90,7 @@ struct hg_ctx {
     int n_cu = 0;
     int32_t kernel = HG_KERNEL_MEGA_REGEN, block = 128, counters_on = 1, timing = 0, refill = 32;
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
+    int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
 };
 
 namespace {
@@ -390,7 +395,7 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -697,6 +702,10 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.n_ranks = c->n_ranks;
     kp.n_local_tiles = c->n_local_tiles;
     kp.stack_depth = c->stack_depth;
+    // deep BLAS (the dragon: 32 levels) descend in long, uneven runs: let the last few lanes pause while the rest
+    // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweep28-29.txt)
+    kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
+                                     : (c->stack_depth > HG_DESCENT_DEEP + 2 ? uint32_t(HG_DESCENT_T) : 0u);
     kp.refill_min = uint32_t(c->refill);
     kp.cube_size = c->cube_size;
     kp.cube_mips = c->cube_mips;
@@ -732,12 +741,14 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
     const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
-        const bool regen = (c->kernel == HG_KERNEL_MEGA_REGEN || c->kernel == HG_KERNEL_MEGA_STREAM) &&
+        const bool regen = (c->kernel == HG_KERNEL_MEGA_REGEN || c->kernel == HG_KERNEL_MEGA_STREAM ||
+                            c->kernel == HG_KERNEL_MEGA_POOL) &&
                            p.halogenDebugMode == 0 &&
                            kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweep12.txt), 256 for the lockstep one
-        const int mblock = c->block == 128 ? (regen ? 64 : 256) : c->block;
+        const bool pool_k = regen && c->kernel == HG_KERNEL_MEGA_POOL;
+        const int mblock = pool_k ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
         // about 16x as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
@@ -745,11 +756,13 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         // rank's share at N=8 314 -> 1212.
         const bool stream_k = c->kernel == HG_KERNEL_MEGA_STREAM;
         const int64_t tiles = c->n_local_tiles;
-        const int64_t resident = int64_t(c->n_cu) * 4 * HG_MEGA_WAVES;  // wave slots of the regen kernel
+        // work units: one tile per wave (regen / stream), HG_POOL_TILES tiles per wave (pool)
+        const int64_t units = pool_k ? (tiles + hg_pool_tiles() - 1) / hg_pool_tiles() : tiles;
+        const int64_t resident = int64_t(c->n_cu) * 4 * (pool_k ? HG_POOL_WAVES : HG_MEGA_WAVES);
         int split = 1;
         if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
-            else split = int(std::min<int64_t>(n_frames, (16 * resident + tiles - 1) / tiles));
+            else split = int(std::min<int64_t>(n_frames, (16 * resident + units - 1) / units));
         }
         int chunk_max = HG_REGEN_MAX_CHUNK;
         if (split > 1) {
@@ -760,7 +773,14 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 return rc;
             }
         }
-        const int mgrid = int((tiles * split + mblock / 64 - 1) / (mblock / 64));
+        const int mgrid = int((units * split + mblock / 64 - 1) / (mblock / 64));
+        if (pool_k) {
+            if (int rc = ensure(c, c->pool, size_t(mgrid) * hg_pool_slots() * 8 * sizeof(float4))) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+            kp.pool = static_cast<float4*>(c->pool.p);
+        }
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
         if (kp.stack_depth > HG_MEGA_LDS_STACK) {  // stack entries beyond the LDS part: one column per thread
             if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - HG_MEGA_LDS_STACK) * 4)) {
@@ -778,8 +798,9 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
-                e = stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
-                             : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
+                    : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
+                               : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
                 if (e == hipSuccess && kc.frame_split > 1) e = hg_launch_blend_frames(kc, c->stream);
                 done += kc.n_frames;
             }
@@ -895,7 +916,7 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     switch (option) {
         case HG_OPT_KERNEL:
             if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
-                value != HG_KERNEL_MEGA_STREAM)
+                value != HG_KERNEL_MEGA_STREAM && value != HG_KERNEL_MEGA_POOL)
                 return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
             c->kernel = value;
             return HG_OK;
@@ -912,6 +933,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_REFILL:
             if (value < 1 || value > 64) return fail(c, HG_E_INVALID, "refill must be 1..64");
             c->refill = value;
+            return HG_OK;
+        case HG_OPT_DESCENT_T:
+            if (value < -1 || value > 64) return fail(c, HG_E_INVALID, "descent threshold must be -1 (auto)..64");
+            c->descent_t = value;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

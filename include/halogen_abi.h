@@ -169,15 +169,22 @@ enum {
  *   queue round trips cost more than the lane utilisation they recover). */
 /* MEGA_STREAM: MEGA_REGEN with a resumable traversal — lanes that finished traversing shade and start their next
  *   ray while the stragglers keep traversing (same limits and fallback as MEGA_REGEN). */
-enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3 };
+/* MEGA_POOL: each wave owns several tiles' paths (more paths than lanes) in a slot array and alternates a trace
+ *   phase (lanes refill from a queue of ready rays as their traversal finishes) with a shade phase (same limits and
+ *   fallback as MEGA_REGEN). */
+enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
+       HG_KERNEL_MEGA_POOL = 4 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).
  * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then
  *   blended in frame order, bit-identical): 0 = automatic (about 16 launches' worth of the GPU's wave slots per
- *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile. */
+ *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile.
+ * HG_OPT_DESCENT_T: traversal descent loop, leave it once at most this many lanes are still descending (the others
+ *   test their leaves meanwhile; each lane's own step order is unchanged): -1 = automatic (3 for BLAS deeper than
+ *   16 levels, else 0 = classic while-while), 0..64 = fixed. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-       HG_OPT_FRAME_SPLIT = 6 };
+       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7 };
 
 int hg_abi_version(void);
 

@@ -16,7 +16,7 @@ REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a di
 
 
 KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN,
-           "stream": abi.HG_KERNEL_MEGA_STREAM}
+           "stream": abi.HG_KERNEL_MEGA_STREAM, "pool": abi.HG_KERNEL_MEGA_POOL}
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
@@ -192,3 +192,20 @@ def test_gpu_frame_parallel_split_bit_exact(gpu, split):
         ctx.set_option(abi.HG_OPT_FRAME_SPLIT, split)
         img, _ = gpu_render(*cases.setup("c1_64")[:2], 8, True, None, ctx=ctx, kernel="regen")
     assert_bitwise(img, ref, f"split {split} vs oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", [1, 4, 63])
+@pytest.mark.parametrize("kernel", ["regen", "mega"])
+def test_gpu_relaxed_descent_bit_exact(gpu, t, kernel):
+    """Leaving the descent loop with up to t lanes still descending (they pause while the others test their leaves)
+    keeps every lane's step order: golden images and counters are unchanged (including the deep dragon BLAS)."""
+    for name in ("c1_64", "dragon1_64x36", "glass_64x36", "c1_32_tritests"):
+        meta = json.loads((GOLD / f"{name}.json").read_text())
+        packed, params, cube, frames, acc = cases.setup(name)
+        with abi.Context(0) as ctx:
+            ctx.set_option(abi.HG_OPT_DESCENT_T, t)
+            img, cnt = gpu_render(packed, params, frames, acc, cube, ctx=ctx, kernel=kernel)
+        assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name} descent_t={t}")
+        for k, v in meta["counters"].items():
+            assert cnt[k] == v, (name, k, cnt[k], v)

@@ -11,7 +11,7 @@ while read -r line; do
   for w in $line; do
     if [[ "$w" == *=* && "$w" != --* ]]; then envs+=("$w"); else args+=("$w"); fi
   done
-  env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline "${args[@]}" > gpurun_out/sweep_one.json 2> gpurun_out/sweep_one.err
+  env "${envs[@]}" timeout -k 10 ${SWEEP_TIMEOUT:-300} python bench.py --no-cpu-baseline "${args[@]}" > gpurun_out/sweep_one.json 2> gpurun_out/sweep_one.err
   rc=$?
   if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $line"; tail -5 gpurun_out/sweep_one.err; exit $rc; fi
   python3 -c "
