@@ -446,46 +446,31 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             }
         }
 #endif
-        if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order
+        if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order (:404-420)
             const uint2 leaf = leaf_range(kp, node);
-            uint32_t ti = leaf.x;
             const uint32_t end = leaf.x + leaf.y;
-#if HG_TRI_PREFETCH
-            float4 ta = ld_off(kp.tri_a, ti << 4), tb = ld_off(kp.tri_b, ti << 4);
-            float tc = ld_off(kp.tri_c, ti << 2);
-#endif
-            for (; ti < end; ++ti) {
+            for (uint32_t ti = leaf.x; ti < end; ++ti) {
                 c.tri_rounds += wave_once();
-#if HG_TRI_PREFETCH
-                const float4 a = ta, b = tb;
-                const float cz = tc;
-                if (ti + 1 < end) {
-                    ta = ld_off(kp.tri_a, (ti + 1) << 4);
-                    tb = ld_off(kp.tri_b, (ti + 1) << 4);
-                    tc = ld_off(kp.tri_c, (ti + 1) << 2);
+                const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+                const float cz = ld_off(kp.tri_c, ti << 2);
+                c.tri++;
+                float t, U, V;
+                bool front;
+                if (tri_accept(lo, ld, a, b, cz, best_t, t, U, V, front)) {
+                    best_t = t;
+                    best_u = U;
+                    best_v = V;
+                    best_tri = ti | (front ? 0u : 0x80000000u);
+                    best_mesh = int(mi);
                 }
-#else
-                    const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-                    const float cz = ld_off(kp.tri_c, ti << 2);
-#endif
-                    c.tri++;
-                    float t, U, V;
-                    bool front;
-                    if (tri_accept(lo, ld, a, b, cz, best_t, t, U, V, front)) {
-                        best_t = t;
-                        best_u = U;
-                        best_v = V;
-                        best_tri = ti | (front ? 0u : 0x80000000u);
-                        best_mesh = int(mi);
-                    }
-                }
-                node = sp > 0 ? stk.pop(sp) : HG_NONE;
             }
-            if (active && node == HG_NONE) {  // this mesh is done: the lane's next live mesh
-                mi = next_live_mesh(live, mi + 1u, nm);
-                if (mi < nm) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
-                else active = false;
-            }
+            node = sp > 0 ? stk.pop(sp) : HG_NONE;
+        }
+        if (active && node == HG_NONE) {  // this mesh is done: the lane's next live mesh
+            mi = next_live_mesh(live, mi + 1u, nm);
+            if (mi < nm) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
+            else active = false;
+        }
     }
 #else
     for (int mi = 0; mi < kp.n_meshes; ++mi) {
