@@ -611,7 +611,10 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
 template <class Stk>
 __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
                                           const Stk& stk, bool act) {
-    while (__any(act && !(t.node & HG_LEAF_BIT))) {
+    for (;;) {  // relaxed while-while, as in isect_meshes
+        const uint32_t n_desc = uint32_t(__popcll(__ballot(act && !(t.node & HG_LEAF_BIT))));
+        if (n_desc == 0u) break;
+        if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(act)))) break;
         c.node_rounds += wave_once();
         if (act && !(t.node & HG_LEAF_BIT)) {
             const uint32_t ro = t.node << 6;
@@ -629,7 +632,7 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
         }
     }
-    if (act && t.node != HG_NONE) {  // :404-420
+    if (act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
         for (uint32_t ti = leaf.x; ti < end; ++ti) {

@@ -174,7 +174,10 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                     head = (n_list - head < took) ? n_list : head + took;
                 }
                 if (!__any(act)) break;
-                while (__any(act && !(node & HG_LEAF_BIT))) {  // descend until every lane is at a leaf
+                for (;;) {  // relaxed while-while, as in isect_meshes
+                    const uint32_t n_desc = uint32_t(__popcll(__ballot(act && !(node & HG_LEAF_BIT))));
+                    if (n_desc == 0u) break;
+                    if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(act)))) break;
                     c.node_rounds += wave_once();
                     if (act && !(node & HG_LEAF_BIT)) {
                         const uint32_t ro = node << 6;
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                         }
                     }
                 }
-                if (act && node != HG_NONE) {  // leaf (:404-420)
+                if (act && node != HG_NONE && (node & HG_LEAF_BIT)) {  // leaf (:404-420)
                     const uint2 leaf = leaf_range(kp, node);
                     const uint32_t end = leaf.x + leaf.y;
                     for (uint32_t ti = leaf.x; ti < end; ++ti) {
