@@ -39,7 +39,9 @@ from halogen import render_pass as rp  # noqa: E402
 from halogen import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
-KERNEL_SYMBOL = {"pool": "hg_trace_pool_kernel", "stream": "hg_trace_stream_kernel", "regen": "hg_trace_regen_kernel", "mega": "hg_trace_kernel", "wavefront": "hg_wf_trace"}
+KERNEL_SYMBOL = {abi.HG_KERNEL_MEGA_POOL: "hg_trace_pool_kernel", abi.HG_KERNEL_MEGA_STREAM: "hg_trace_stream_kernel",
+                 abi.HG_KERNEL_MEGA_REGEN: "hg_trace_regen_kernel", abi.HG_KERNEL_MEGA: "hg_trace_kernel",
+                 abi.HG_KERNEL_WAVEFRONT: "hg_wf_trace"}
 METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
 
 
@@ -87,7 +89,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="regen", choices=["wavefront", "mega", "regen", "stream", "pool"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
                     help="progressive 1-spp frames per step per GPU-equivalent (64 = one C3 image)")
     ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
@@ -136,7 +138,8 @@ def main():
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
 
     ctx = abi.Context(device)
-    ctx.set_option(abi.HG_OPT_KERNEL, {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA,
+    ctx.set_option(abi.HG_OPT_KERNEL, {"auto": abi.HG_KERNEL_AUTO, "wavefront": abi.HG_KERNEL_WAVEFRONT,
+                                       "mega": abi.HG_KERNEL_MEGA,
                                        "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
                                        "pool": abi.HG_KERNEL_MEGA_POOL}[args.kernel])
     if args.timing:
@@ -193,6 +196,7 @@ def main():
     dt = time.perf_counter() - t0
 
     timing = ctx.counters()  # kernel_ms / launches of the timed launches
+    kernel_symbol = KERNEL_SYMBOL.get(int(timing["last_kernel"]), "?")  # the variant HG_KERNEL_AUTO resolved to
     replay_identical = None
     timed_img = ctx.readback(W, H) if world == 1 and (not args.no_counters or args.save_image) else None
     if not args.no_counters:
@@ -238,7 +242,7 @@ def main():
             try:
                 t = json.loads(tfile.read_text())
                 if (t.get("config") == args.config and t.get("width") == W and t.get("height") == H
-                        and t.get("frames_per_launch") == frames_per_step and t.get("kernel") == KERNEL_SYMBOL[args.kernel] + "<false>"):
+                        and t.get("frames_per_launch") == frames_per_step and t.get("kernel") == kernel_symbol + "<false>"):
                     traffic = t.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -263,7 +267,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_launch_ms": mean_launch_s * 1e3,
-                         "kernel": KERNEL_SYMBOL[args.kernel]},
+                         "kernel": kernel_symbol},
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "counting_replay_bit_identical": replay_identical,

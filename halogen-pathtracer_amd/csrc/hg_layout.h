@@ -48,8 +48,11 @@
 #ifndef HG_MEGA_WAVES
 #define HG_MEGA_WAVES 6  // regenerating megakernel: waves/SIMD target
 #endif
+#ifndef HG_STREAM_WAVES
+#define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~120 VGPRs)
+#endif
 #ifndef HG_STREAM_TMIN
-#define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing
+#define HG_STREAM_TMIN 8  // streaming kernel: shade once at most this many lanes are still traversing
 #endif
 #ifndef HG_RCP_NORMALIZE
 #define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)

@@ -272,7 +272,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
 template <bool kCounters>
-__global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
+__global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);

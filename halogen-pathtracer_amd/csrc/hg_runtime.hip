@@ -88,7 +88,7 @@ struct hg_ctx {
 
     // device / options
     int n_cu = 0;
-    int32_t kernel = HG_KERNEL_MEGA_REGEN, block = 128, counters_on = 1, timing = 0, refill = 32;
+    int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0, refill = 32;
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
     int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
 };
@@ -739,26 +739,32 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (int rc = event_pair(c, ev)) return rc;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
-    const bool mega = c->kernel != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
+    // HG_KERNEL_AUTO: the streaming kernel for deep BLAS (its resumable traversal pays off when a few lanes carry
+    // long traversals: C3 +6 %), the regenerating kernel otherwise (C2/C5: stream -18/-20 %) (tools/sweep35.txt)
+    const bool deep_blas = c->stack_depth > HG_DESCENT_DEEP + 2;
+    const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (deep_blas ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
+                                                     : c->kernel;
+    const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     if (mega) {
-        const bool regen = (c->kernel == HG_KERNEL_MEGA_REGEN || c->kernel == HG_KERNEL_MEGA_STREAM ||
-                            c->kernel == HG_KERNEL_MEGA_POOL) &&
+        const bool regen = (kern == HG_KERNEL_MEGA_REGEN || kern == HG_KERNEL_MEGA_STREAM ||
+                            kern == HG_KERNEL_MEGA_POOL) &&
                            p.halogenDebugMode == 0 &&
                            kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweep12.txt), 256 for the lockstep one
-        const bool pool_k = regen && c->kernel == HG_KERNEL_MEGA_POOL;
+        const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
         const int mblock = pool_k ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
         // about 16x as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
         // (bit-identical).  Measured (tools/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
         // rank's share at N=8 314 -> 1212.
-        const bool stream_k = c->kernel == HG_KERNEL_MEGA_STREAM;
+        const bool stream_k = regen && kern == HG_KERNEL_MEGA_STREAM;
         const int64_t tiles = c->n_local_tiles;
         // work units: one tile per wave (regen / stream), HG_POOL_TILES tiles per wave (pool)
         const int64_t units = pool_k ? (tiles + hg_pool_tiles() - 1) / hg_pool_tiles() : tiles;
-        const int64_t resident = int64_t(c->n_cu) * 4 * (pool_k ? HG_POOL_WAVES : HG_MEGA_WAVES);
+        const int64_t resident =
+            int64_t(c->n_cu) * 4 * (pool_k ? HG_POOL_WAVES : stream_k ? HG_STREAM_WAVES : HG_MEGA_WAVES);
         int split = 1;
         if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
@@ -790,6 +796,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             kp.spill = static_cast<uint32_t*>(c->wf_spill.p);
         }
 
+        c->counters.last_kernel = uint64_t(regen ? kern : HG_KERNEL_MEGA);
         hipError_t e = hipSuccess;
         if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
             HgKernelParams kc = kp;
@@ -811,9 +818,12 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             c->free_events.push_back(ev);
             return fail(c, HG_E_HIP, "megakernel launch failed: %s", hipGetErrorString(e));
         }
-    } else if (int rc = render_wavefront(c, kp)) {
-        c->free_events.push_back(ev);
-        return rc;
+    } else {
+        c->counters.last_kernel = HG_KERNEL_WAVEFRONT;
+        if (int rc = render_wavefront(c, kp)) {
+            c->free_events.push_back(ev);
+            return rc;
+        }
     }
     HG_HIP(c, hipEventRecord(ev.second, c->stream));
     c->pending.push_back(ev);
@@ -916,7 +926,7 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     switch (option) {
         case HG_OPT_KERNEL:
             if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
-                value != HG_KERNEL_MEGA_STREAM && value != HG_KERNEL_MEGA_POOL)
+                value != HG_KERNEL_MEGA_STREAM && value != HG_KERNEL_MEGA_POOL && value != HG_KERNEL_AUTO)
                 return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
             c->kernel = value;
             return HG_OK;

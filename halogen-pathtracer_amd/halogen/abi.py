@@ -79,7 +79,7 @@ class HgCounters(C.Structure):
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
                 ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
-                ("tri_rounds", C.c_uint64)]
+                ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -87,6 +87,7 @@ class HgCounters(C.Structure):
 
 HG_OK = 0
 HG_KERNEL_MEGA, HG_KERNEL_WAVEFRONT, HG_KERNEL_MEGA_REGEN, HG_KERNEL_MEGA_STREAM, HG_KERNEL_MEGA_POOL = 0, 1, 2, 3, 4
+HG_KERNEL_AUTO = 5
 HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING, HG_OPT_REFILL, HG_OPT_FRAME_SPLIT = 1, 2, 3, 4, 5, 6
 HG_OPT_DESCENT_T = 7
 

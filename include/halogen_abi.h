@@ -146,6 +146,7 @@ typedef struct hg_counters {
     uint64_t node_rounds;  /* megakernels: wave-level iterations of the BVH descent loop (SIMD utilisation of the
                               descent = aabb_tests / 2 / (64 * node_rounds)) */
     uint64_t tri_rounds;   /* megakernels: wave-level iterations of the leaf loop (tri_tests / (64 * tri_rounds)) */
+    uint64_t last_kernel;  /* HG_KERNEL_* variant the last hg_render ran (AUTO resolved; debug views: MEGA) */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -161,7 +162,7 @@ enum {
 };
 
 /* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v); all produce bit-identical images.
- * MEGA_REGEN (default): one lane per pixel of an 8x8-tile wave, one bounce per loop iteration; a lane whose path
+ * MEGA_REGEN: one lane per pixel of an 8x8-tile wave, one bounce per loop iteration; a lane whose path
  *   ends starts its next sample / frame at once (per-lane path regeneration), so no lane idles until the
  *   longest path of its wave ends.  Falls back to MEGA when maxBounces > 250 or samplesPerPixel >= 65535.
  * MEGA: the lockstep form — each lane traces whole paths, frame after frame (also runs the debug views 1-5).
@@ -172,8 +173,9 @@ enum {
 /* MEGA_POOL: each wave owns several tiles' paths (more paths than lanes) in a slot array and alternates a trace
  *   phase (lanes refill from a queue of ready rays as their traversal finishes) with a shade phase (same limits and
  *   fallback as MEGA_REGEN). */
+/* AUTO (default): MEGA_STREAM when the scene has a BLAS deeper than 16 levels, else MEGA_REGEN. */
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
-       HG_KERNEL_MEGA_POOL = 4 };
+       HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5 };
 /* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).

@@ -16,7 +16,7 @@ REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a di
 
 
 KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN,
-           "stream": abi.HG_KERNEL_MEGA_STREAM, "pool": abi.HG_KERNEL_MEGA_POOL}
+           "stream": abi.HG_KERNEL_MEGA_STREAM, "pool": abi.HG_KERNEL_MEGA_POOL, "auto": abi.HG_KERNEL_AUTO}
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
@@ -209,3 +209,22 @@ def test_gpu_relaxed_descent_bit_exact(gpu, t, kernel):
         assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name} descent_t={t}")
         for k, v in meta["counters"].items():
             assert cnt[k] == v, (name, k, cnt[k], v)
+
+
+@pytest.mark.gpu
+def test_gpu_auto_kernel_choice(gpu):
+    """HG_KERNEL_AUTO (the default) runs the streaming kernel for deep BLAS (the 871k dragon) and the regenerating
+    kernel for shallow scenes; the debug views always run the lockstep kernel."""
+    with abi.Context(0) as ctx:
+        assert ctx.counters()["last_kernel"] == 0
+    for name, want in (("c1_64", abi.HG_KERNEL_MEGA_REGEN), ("glass_64x36", abi.HG_KERNEL_MEGA_REGEN),
+                       ("c1_32_normal", abi.HG_KERNEL_MEGA)):
+        packed, params, cube, frames, acc = cases.setup(name)
+        _, cnt = gpu_render(packed, params, frames, acc, cube, kernel="auto")
+        assert cnt["last_kernel"] == want, (name, cnt["last_kernel"])
+    cfg = scenes.CONFIGS["C3"].resized(64, 64, 1)
+    packed = cases._scene("dragon", 10)
+    s = rp.clamp_settings(scenes.settings_for(cfg))
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), False)
+    _, cnt = gpu_render(packed, params, 2, True, None, kernel="auto")
+    assert cnt["last_kernel"] == abi.HG_KERNEL_MEGA_STREAM
