@@ -274,6 +274,8 @@ def main():
             "simd_utilisation": {"descent": cnt["aabb_tests"] / 2 / max(64 * cnt["node_rounds"], 1),
                                  "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1)} if counters_ok else None,
             "emulated_ranks": emu or None,
+            # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
+            "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},

@@ -876,6 +876,7 @@ int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
     const size_t need = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     if (n_bytes < need) return fail(c, HG_E_INVALID, "destination too small (%zu < %zu)", n_bytes, need);
     if (int rc = set_device(c)) return rc;
+    HG_HIP(c, hipStreamSynchronize(c->stream));  // every render kernel retired before the copy engine reads acc
     if (need) HG_HIP(c, hipMemcpyAsync(dst, c->acc.p, need, hipMemcpyDeviceToDevice, c->stream));
     HG_HIP(c, hipStreamSynchronize(c->stream));
     return drain_events(c);
