@@ -1,0 +1,103 @@
+// HalogenNative.cs — P/Invoke binding of libhalogen_hip.so (include/halogen_abi.h) for the reference's C# host.
+//
+// Drop next to Assets/Scripts/Render Features/HalogenRenderPass.cs.  The scene structs (HalogenSphere,
+// HalogenMeshData, PackedHalogenMaterial, HalogenTriangle, BVHEntry) are the reference's own
+// [StructLayout(LayoutKind.Sequential)] structs (HalogenRenderPass.cs:10-76) and are passed unchanged; only the
+// uniform block and the counters are new.  INTEGRATION.md §2 lists the call-site changes in HalogenRenderPass.
+// tests/test_csharp_binding.py checks this file against the C header (every export declared, struct fields in
+// order with matching types).  There is no C# toolchain in the build image, so it is not compiled here.
+using System;
+using System.Runtime.InteropServices;
+using UnityEngine;
+
+public static class HalogenNative
+{
+    const string Lib = "halogen_hip";
+
+    // hg_params: every uniform of HalgoenCompute.compute:26-68,185 as DispatchHalogenTrace sets it (RP:359-401)
+    [StructLayout(LayoutKind.Sequential)]
+    public struct HgParams
+    {
+        public Matrix4x4 camLocalToWorld;     // hg_mat4: Unity column-major m00,m10,...
+        public Vector4 screenParameters;      // (pixelWidth, pixelHeight, 0, 0)
+        public Vector4 viewParameters;        // (w, h, near, far)
+        public Vector4 cameraParameters;      // camera position (dead in the kernel)
+        public int frameCount;                // FrameCount of the first traced frame
+        public uint samplesPerPixel;
+        public uint maxBounces;
+        public uint maxDiffuseBounces;
+        public uint maxGlossyBounces;
+        public uint maxTransmissionBounces;
+        public uint halogenDebugMode;
+        public uint triangleDebugDisplayRange;
+        public uint boxDebugDisplayRange;
+        public int defaultHDRIMipLevel;
+        public float focalPlaneDistance;
+        public float focalConeAngle;
+        public float filterRadius;
+        public int useEnvironmentCubemap;
+        public Vector4 bufferCounts;          // (spheres, meshes, 0, 0)
+    }
+
+    [StructLayout(LayoutKind.Sequential)]
+    public struct HgCounters
+    {
+        public ulong paths;
+        public ulong rays;
+        public ulong tri_tests;
+        public ulong aabb_tests;
+        public ulong mesh_visits;
+        public ulong sphere_tests;
+        public ulong hits;
+        public double kernel_ms;
+        public ulong launches;
+        public double trace_ms;
+        public ulong trace_launches;
+        public ulong node_rounds;
+        public ulong tri_rounds;
+        public ulong last_kernel;
+    }
+
+    public const int HG_OK = 0;
+    public const int HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
+                     HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
+    public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
+                     HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7;
+    public const int HG_SELFTEST_RCP = 1;
+
+    [DllImport(Lib)] public static extern int hg_abi_version();
+    [DllImport(Lib)] public static extern int hg_create(int device, out IntPtr ctx);
+    [DllImport(Lib)] public static extern void hg_destroy(IntPtr ctx);
+    [DllImport(Lib)] public static extern IntPtr hg_last_error(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_upload_scene(IntPtr ctx,
+        HalogenSphere[] spheres, int nSpheres, HalogenMeshData[] meshes, int nMeshes,
+        PackedHalogenMaterial[] materials, int nMaterials, HalogenTriangle[] triangles, int nTriangles,
+        BVHEntry[] blas, int nNodes);
+    [DllImport(Lib)] public static extern int hg_upload_cubemap(IntPtr ctx, int faceSize, int nMips, float[] texels,
+        UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_set_params(IntPtr ctx, ref HgParams p);
+    [DllImport(Lib)] public static extern int hg_resize(IntPtr ctx, int width, int height);
+    [DllImport(Lib)] public static extern int hg_set_tiling(IntPtr ctx, int rank, int nRanks);
+    [DllImport(Lib)] public static extern int hg_clear_accumulation(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_render(IntPtr ctx, int nFrames, int accumulate);
+    [DllImport(Lib)] public static extern int hg_synchronize(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_readback(IntPtr ctx, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_copy_tiles_device(IntPtr ctx, IntPtr dstDevice, UIntPtr nBytes);
+    [DllImport(Lib)] public static extern int hg_local_tile_count(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_get_counters(IntPtr ctx, out HgCounters c);
+    [DllImport(Lib)] public static extern int hg_reset_counters(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_set_option(IntPtr ctx, int option, int value);
+    [DllImport(Lib)] public static extern long hg_selftest(IntPtr ctx, int test, out long tested);
+    [DllImport(Lib)] public static extern long hg_build_blas(float[] vertices, int nVertices, int[] indices, int nTris,
+        float[] rootMin, float[] rootMax, int maxHierarchyDepth, [Out] BVHEntry[] outNodes, long maxNodes);
+    [DllImport(Lib)] public static extern void hg_unity_bounds(float[] inMin, float[] inMax, int padIfThin,
+        [Out] float[] outMin, [Out] float[] outMax);
+    [DllImport(Lib)] public static extern int hg_pack_triangles(float[] vertices, float[] normals, int nVertices,
+        int[] indices, int nTris, [Out] HalogenTriangle[] outTriangles);
+
+    public static void Check(IntPtr ctx, int rc, string what)
+    {
+        if (rc != HG_OK)
+            throw new Exception($"{what} failed ({rc}): {Marshal.PtrToStringAnsi(hg_last_error(ctx))}");
+    }
+}
