@@ -63,6 +63,9 @@
 #ifndef HG_DESCENT_T
 #define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
 #endif
+#ifndef HG_STREAM_DESCENT_T
+#define HG_STREAM_DESCENT_T 4  // the same for the streaming kernel
+#endif
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16
 #endif

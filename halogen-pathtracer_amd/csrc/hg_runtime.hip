@@ -704,8 +704,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.stack_depth = c->stack_depth;
     // deep BLAS (the dragon: 32 levels) descend in long, uneven runs: let the last few lanes pause while the rest
     // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweep28-29.txt)
-    kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
-                                     : (c->stack_depth > HG_DESCENT_DEEP + 2 ? uint32_t(HG_DESCENT_T) : 0u);
+
     kp.refill_min = uint32_t(c->refill);
     kp.cube_size = c->cube_size;
     kp.cube_mips = c->cube_mips;
@@ -745,6 +744,11 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (deep_blas ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
                                                      : c->kernel;
     const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
+    // relaxed descent threshold: 3 for the regen / lockstep kernels, 4 for the streaming one (tools/sweep38.txt)
+    kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
+                   : !deep_blas      ? 0u
+                   : kern == HG_KERNEL_MEGA_STREAM ? uint32_t(HG_STREAM_DESCENT_T)
+                                                   : uint32_t(HG_DESCENT_T);
     if (mega) {
         const bool regen = (kern == HG_KERNEL_MEGA_REGEN || kern == HG_KERNEL_MEGA_STREAM ||
                             kern == HG_KERNEL_MEGA_POOL) &&
