@@ -579,7 +579,7 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
 // between steps (other lanes shade) and resume.  Same visit order, same counters, same result.
 // ---------------------------------------------------------------------------------------------------
 struct Trav {
-    f3 lo, ld, inv;        // ray in the current mesh's local space, 1/ld
+    f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
     uint32_t best_tri;     // triangle | orientation<0 << 31, HG_NONE: no mesh hit yet
     uint32_t best_mesh, sph, node, sp, mi;  // mi == n_meshes: traversal finished
@@ -603,7 +603,8 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     t.node = HG_NONE;
     const uint32_t nm = uint32_t(kp.n_meshes);
     t.mi = next_live_mesh(t.live, 0u, nm);
-    if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, t.inv, t.node);
+    f3 inv;
+    if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv, t.node);
 }
 
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
@@ -611,6 +612,9 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
 template <class Stk>
 __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
                                           const Stk& stk, bool act) {
+    // 1/ld (the same rcp_exact values mesh_local_ray computes) is not kept in Trav: live only during this round, it
+    // stays out of the registers held across the streaming kernel's shading code
+    const f3 inv = mk(rcp_exact(t.ld.x), rcp_exact(t.ld.y), rcp_exact(t.ld.z));
     for (;;) {  // relaxed while-while, as in isect_meshes
         const uint32_t n_desc = uint32_t(__popcll(__ballot(act && !(t.node & HG_LEAF_BIT))));
         if (n_desc == 0u) break;
@@ -620,8 +624,8 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             const uint32_t ro = t.node << 6;
             const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
                          b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
-            const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), t.lo, t.inv);
-            const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), t.lo, t.inv);
+            const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), t.lo, inv);
+            const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), t.lo, inv);
             c.aabb += 2;
             const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
             const bool bFirst = dB < dA;  // :430-444
@@ -655,7 +659,8 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     if (act && t.node == HG_NONE) {
         const uint32_t nm = uint32_t(kp.n_meshes);
         t.mi = next_live_mesh(t.live, t.mi + 1u, nm);
-        if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, t.inv, t.node);
+        f3 inv_next;
+        if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv_next, t.node);
     }
 }
 
