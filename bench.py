@@ -273,6 +273,14 @@ def main():
             "counting_replay_bit_identical": replay_identical,
             "simd_utilisation": {"descent": cnt["aabb_tests"] / 2 / max(64 * cnt["node_rounds"], 1),
                                  "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1)} if counters_ok else None,
+            # wave-clock split of the counting replay (regenerating / streaming megakernels)
+            "phase_split": {"traversal": cnt["trace_cycles"] / (cnt["trace_cycles"] + cnt["shade_cycles"]),
+                            "shading": cnt["shade_cycles"] / (cnt["trace_cycles"] + cnt["shade_cycles"])}
+            if counters_ok and cnt.get("trace_cycles", 0) + cnt.get("shade_cycles", 0) > 0 else None,
+            # analysis builds (HG_PHASE_DETAIL=1): the shading phase split further, as fractions of all wave cycles
+            "shading_detail": dict(zip(("hit_resolve", "material_bsdf", "path_end_camera", "next_ray_setup"),
+                                       (x / (cnt["trace_cycles"] + cnt["shade_cycles"]) for x in cnt["shade_detail"])))
+            if counters_ok and any(cnt.get("shade_detail", [])) else None,
             "emulated_ranks": emu or None,
             # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
             "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,

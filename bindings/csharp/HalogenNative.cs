@@ -56,6 +56,9 @@ public static class HalogenNative
         public ulong node_rounds;
         public ulong tri_rounds;
         public ulong last_kernel;
+        public ulong trace_cycles;
+        public ulong shade_cycles;
+        [MarshalAs(UnmanagedType.ByValArray, SizeConst = 4)] public ulong[] shade_detail;
     }
 
     public const int HG_OK = 0;

@@ -124,6 +124,21 @@ struct Counters {
     uint32_t rays, tri, aabb, node_rounds, tri_rounds, hits;  // *_rounds: wave-level loop iterations (one lane counts)
 };
 // 1 in exactly one active lane (the lowest): summed over lanes, counts the wave-level executions of a code point
+// Wave clock (s_memtime) for the counting instantiations' phase split; volatile + memory clobber keep the
+// compiler from moving it across the code it brackets.
+__device__ __forceinline__ uint64_t wave_clock() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
+}
+// HG_PHASE_DETAIL analysis builds: add the wave clock elapsed since `since` to counter slot `slot` (from the first
+// active lane, so it works inside divergent code) and return the new clock.
+__device__ __forceinline__ uint64_t phase_mark(const HgKernelParams& kp, int slot, uint64_t since) {
+    const uint64_t t = wave_clock();
+    if (int(threadIdx.x & 63u) == __ffsll((unsigned long long)__ballot(1)) - 1)
+        atomicAdd(kp.counters + slot, (unsigned long long)(t - since));
+    return wave_clock();
+}
 __device__ __forceinline__ uint32_t wave_once() {
     return __lane_id() == uint32_t(__builtin_ctzll(__ballot(1))) ? 1u : 0u;
 }
@@ -199,6 +214,16 @@ __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
+// Load of scene data the kernel never writes (mesh records, spheres) through the constant address space: a
+// wave-uniform address then compiles to a scalar load (s_load_dwordx4, scalar cache) even after the kernel's own
+// global stores, where a generic load must stay a vector load (one full memory latency per mesh / sphere).
+typedef float hg_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldc(const float4* base, uint32_t i) {
+    typedef const __attribute__((address_space(4))) hg_v4f* cptr;
+    const hg_v4f v = ((cptr)(uintptr_t)base)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint2 leaf_range(const HgKernelParams& kp, uint32_t ref) {
     const uint32_t cnt = (ref >> HG_LEAF_CNT_SHIFT) & HG_LEAF_INLINE_MAX;
     if (__builtin_expect(cnt != 0u, 1)) return make_uint2(ref & HG_LEAF_PAYLOAD, cnt);
@@ -224,9 +249,9 @@ __device__ uint32_t isect_spheres(const HgKernelParams& kp, const Ray& ray, floa
     uint32_t best = HG_NONE;
     f3 inv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     for (int i = 0; i < kp.n_spheres; ++i) {
-        const float4 cr = kp.spheres[3 * i];
-        const float4 am = kp.spheres[3 * i + 1];
-        const float4 b = kp.spheres[3 * i + 2];
+        const float4 cr = ldc(kp.spheres, 3 * i);
+        const float4 am = ldc(kp.spheres, 3 * i + 1);
+        const float4 b = ldc(kp.spheres, 3 * i + 2);
         if (!(ray_aabb(xyz(am), xyz(b), ray.o, inv) < kp.far_)) continue;
         // sphere_intersection :266-303
         f3 center = xyz(cr);
@@ -267,11 +292,16 @@ __device__ __forceinline__ uint64_t mesh_live_mask(const HgKernelParams& kp, f3 
     uint64_t live = ~0ull;
     const float lim = best_t * 1.0001f + 1e-4f;
     const int ncull = kp.n_meshes < 64 ? kp.n_meshes : 64;
+    static_assert(sizeof(HgDevMesh) % 16 == 0 && offsetof(HgDevMesh, cull_a_lo) % 16 == 0, "float4 records");
+    const float4* mrec = reinterpret_cast<const float4*>(kp.meshes);
+    constexpr uint32_t kRec = sizeof(HgDevMesh) / 16, kCull = offsetof(HgDevMesh, cull_a_lo) / 16;
     for (int m = 0; m < ncull; ++m) {
-        const HgDevMesh& md = kp.meshes[m];
-        if (!md.cullable) continue;
-        const float dA = ray_aabb(xyz(md.cull_a_lo), xyz(md.cull_a_hi), wo, winv);
-        const float dB = ray_aabb(xyz(md.cull_b_lo), xyz(md.cull_b_hi), wo, winv);
+        const float4 hdr = ldc(mrec, m * kRec + kCull - 1);  // root_ref, tri_offset, material, cullable
+        if (!__float_as_uint(hdr.w)) continue;
+        const float4 alo = ldc(mrec, m * kRec + kCull), ahi = ldc(mrec, m * kRec + kCull + 1),
+                     blo = ldc(mrec, m * kRec + kCull + 2), bhi = ldc(mrec, m * kRec + kCull + 3);
+        const float dA = ray_aabb(xyz(alo), xyz(ahi), wo, winv);
+        const float dB = ray_aabb(xyz(blo), xyz(bhi), wo, winv);
         const bool farA = dA == HG_INF || dA > lim, farB = dB == HG_INF || dB > lim;  // NaN never skips
         if (farA && farB) {
             live &= ~(1ull << m);
@@ -588,8 +618,14 @@ struct Trav {
 
 __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c) {
     c.rays++;
+#if HG_PHASE_DETAIL == 2
+    uint64_t tp = wave_clock();
+#endif
     t.sph_t = HG_INF;
     t.sph = isect_spheres(kp, ray, t.sph_t);
+#if HG_PHASE_DETAIL == 2
+    if (kp.counters) tp = phase_mark(kp, 11, tp);
+#endif
     t.best_t = t.sph_t;  // closestIntersection.rayT starts at the sphere hit (:381)
     t.best_u = 0.0f;
     t.best_v = 0.0f;
@@ -598,6 +634,9 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     uint32_t culled = 0;
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     t.live = mesh_live_mask(kp, ray.o, winv, t.best_t, culled);
+#if HG_PHASE_DETAIL == 2
+    if (kp.counters) tp = phase_mark(kp, 12, tp);
+#endif
     c.aabb += 2 * culled;
     t.sp = 0;
     t.node = HG_NONE;
@@ -605,6 +644,12 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     t.mi = next_live_mesh(t.live, 0u, nm);
     f3 inv;
     if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv, t.node);
+#if HG_PHASE_DETAIL == 2
+    if (kp.counters) {
+        asm volatile("" : : "v"(t.node), "v"(t.lo.x), "v"(t.ld.x));  // keep the loads' wait inside this phase
+        tp = phase_mark(kp, 13, tp);
+    }
+#endif
 }
 
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that

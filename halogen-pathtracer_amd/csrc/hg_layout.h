@@ -81,6 +81,9 @@
 #ifndef HG_TRI_PREFETCH
 #define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
 #endif
+#ifndef HG_PHASE_DETAIL
+#define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
+#endif
 #ifndef HG_MEGA_LDS_STACK
 #define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
 #endif

@@ -136,9 +136,14 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         s_col.set(mk(0, 0, 0));
         s_sum.set(mk(0, 0, 0));
     }
+    uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
     while (__any(work)) {
+        const uint64_t t0 = kCounters ? wave_clock() : 0;
+        const bool was_work = work;
+        uint64_t t1 = 0;
         if (work) {
             const Hit hit = intersect(kp, ray, c, stk);
+            if (kCounters) t1 = wave_clock();
             bool alive = false;
             f3 thr = s_thr.get(), col = s_col.get();
             if (hit.t < kp.far_) {  // :898-936
@@ -214,6 +219,13 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
             s_thr.set(thr);
             s_col.set(col);
         }
+        if (kCounters) {  // t1 was read inside the divergent branch: take it from a lane that ran it
+            const uint64_t t2 = wave_clock();
+            const int src = __ffsll((unsigned long long)__ballot(was_work)) - 1;
+            const uint64_t t1u = (uint64_t(__shfl(uint32_t(t1 >> 32), src)) << 32) | __shfl(uint32_t(t1), src);
+            cyc_trav += t1u - t0;
+            cyc_shade += t2 - t1u;
+        }
     }
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
@@ -222,6 +234,10 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         for (int k = 0; k < 9; ++k) {
             const uint32_t sv = wave_sum(v[k]);
             if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
+        }
+        if (lane == 0) {
+            atomicAdd(kp.counters + 9, (unsigned long long)cyc_trav);
+            atomicAdd(kp.counters + 10, (unsigned long long)cyc_shade);
         }
     }
 }
@@ -312,8 +328,10 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         s_sum.set(mk(0, 0, 0));
         trav_begin(kp, ray, tv, c);
     }
+    uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
     while (__any(work)) {
         // ---- traversal rounds until few lanes are left traversing
+        if (kCounters) cyc_trav -= wave_clock();
         for (;;) {
             const bool act = work && tv.mi < nm;
             const uint32_t n_act = uint32_t(__popcll(__ballot(act)));
@@ -321,9 +339,20 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             if (n_act <= HG_STREAM_TMIN && __any(work && !act)) break;
             trav_step(kp, ray, tv, c, stk, act);
         }
+        if (kCounters) {
+            const uint64_t t = wave_clock();
+            cyc_trav += t;
+            cyc_shade -= t;
+        }
         // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
         while (work && tv.mi >= nm) {
+#if HG_PHASE_DETAIL == 1
+            uint64_t tp = kCounters ? wave_clock() : 0;
+#endif
             const Hit hit = trav_hit(kp, ray, tv);
+#if HG_PHASE_DETAIL == 1
+            if (kCounters) tp = phase_mark(kp, 11, tp);
+#endif
             bool alive = false;
             f3 thr = s_thr.get(), col = s_col.get();
             if (hit.t < kp.far_) {  // :898-936
@@ -348,6 +377,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             } else {  // :941
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
+#if HG_PHASE_DETAIL == 1
+            if (kCounters) tp = phase_mark(kp, 12, tp);
+#endif
             if (!alive) {
                 f3 sum = s_sum.get() + col;  // RayColor += trace_ray(...)
                 ++fs;
@@ -399,8 +431,15 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             }
             s_thr.set(thr);
             s_col.set(col);
+#if HG_PHASE_DETAIL == 1
+            if (kCounters) tp = phase_mark(kp, 13, tp);
+#endif
             if (alive) trav_begin(kp, ray, tv, c);
+#if HG_PHASE_DETAIL == 1
+            if (kCounters) tp = phase_mark(kp, 14, tp);
+#endif
         }
+        if (kCounters) cyc_shade += wave_clock();
     }
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
@@ -409,6 +448,10 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         for (int k = 0; k < 9; ++k) {
             const uint32_t sv = wave_sum(v[k]);
             if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
+        }
+        if (lane == 0) {
+            atomicAdd(kp.counters + 9, (unsigned long long)cyc_trav);
+            atomicAdd(kp.counters + 10, (unsigned long long)cyc_shade);
         }
     }
 }

@@ -904,6 +904,9 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->hits = v[6];
     out->node_rounds = v[7];
     out->tri_rounds = v[8];
+    out->trace_cycles = v[9];
+    out->shade_cycles = v[10];
+    for (int k = 0; k < 4; ++k) out->shade_detail[k] = v[11 + k];
     return HG_OK;
 }
 

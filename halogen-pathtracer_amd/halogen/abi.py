@@ -79,10 +79,13 @@ class HgCounters(C.Structure):
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
                 ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
-                ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64)]
+                ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64),
+                ("trace_cycles", C.c_uint64), ("shade_cycles", C.c_uint64),
+                ("shade_detail", C.c_uint64 * 4)]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        return {name: (list(v) if isinstance(v, C.Array) else v)
+                for name, v in ((name, getattr(self, name)) for name, _ in self._fields_)}
 
 
 HG_OK = 0

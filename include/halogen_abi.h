@@ -147,6 +147,11 @@ typedef struct hg_counters {
                               descent = aabb_tests / 2 / (64 * node_rounds)) */
     uint64_t tri_rounds;   /* megakernels: wave-level iterations of the leaf loop (tri_tests / (64 * tri_rounds)) */
     uint64_t last_kernel;  /* HG_KERNEL_* variant the last hg_render ran (AUTO resolved; debug views: MEGA) */
+    uint64_t trace_cycles; /* regenerating / streaming megakernels: wave clock cycles (s_memtime) spent in BVH
+                              traversal, summed over waves */
+    uint64_t shade_cycles; /* ... and in the rest of the bounce (shading, sampling, ray generation, accumulation) */
+    uint64_t shade_detail[4]; /* analysis builds (HG_PHASE_DETAIL=1) only, streaming kernel: wave clock cycles of
+                                 hit resolve / material + BSDF / path end + camera ray / next-ray setup; else 0 */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;

@@ -22,7 +22,12 @@ def c_struct(name):
         if not decl:
             continue
         typ, names = decl.split(None, 1)
-        fields += [(typ, n.strip()) for n in names.split(",")]
+        for n in names.split(","):
+            n = n.strip()
+            if "[" in n:  # fixed-size array member: uint64_t x[4] <-> public ulong[] x (ByValArray)
+                fields.append((typ + "[]", n[:n.index("[")]))
+            else:
+                fields.append((typ, n))
     return fields
 
 
@@ -34,6 +39,7 @@ def cs_struct(name):
         decl = decl.strip()
         if not decl:
             continue
+        decl = re.sub(r"^\[MarshalAs\(UnmanagedType\.ByValArray, SizeConst = \d+\)\]\s*", "", decl)
         _, typ, names = decl.split(None, 2)
         fields += [(typ, n.strip()) for n in names.split(",")]
     return fields
@@ -49,7 +55,8 @@ def test_struct_layouts_match_header():
     for c_name, cs_name in (("hg_params", "HgParams"), ("hg_counters", "HgCounters")):
         c_fields, cs_fields = c_struct(c_name), cs_struct(cs_name)
         assert [n for _, n in c_fields] == [n for _, n in cs_fields], c_name
-        assert [C_TO_CS[t] for t, _ in c_fields] == [t for t, _ in cs_fields], c_name
+        cs_type = lambda t: C_TO_CS[t[:-2]] + "[]" if t.endswith("[]") else C_TO_CS[t]
+        assert [cs_type(t) for t, _ in c_fields] == [t for t, _ in cs_fields], c_name
 
 
 def test_constants_match_header():
