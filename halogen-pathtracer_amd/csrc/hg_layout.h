@@ -52,7 +52,7 @@
 #define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~120 VGPRs)
 #endif
 #ifndef HG_STREAM_TMIN
-#define HG_STREAM_TMIN 8  // streaming kernel: shade once at most this many lanes are still traversing
+#define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing (tools/sweep42.txt)
 #endif
 #ifndef HG_RCP_NORMALIZE
 #define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)
@@ -64,7 +64,7 @@
 #define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
 #endif
 #ifndef HG_STREAM_DESCENT_T
-#define HG_STREAM_DESCENT_T 4  // the same for the streaming kernel
+#define HG_STREAM_DESCENT_T 6  // the same for the streaming kernel (tools/sweep42.txt)
 #endif
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16
