@@ -272,7 +272,9 @@ def main():
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
             "counting_replay_bit_identical": replay_identical,
             "simd_utilisation": {"descent": cnt["aabb_tests"] / 2 / max(64 * cnt["node_rounds"], 1),
-                                 "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1)} if counters_ok else None,
+                                 "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1),
+                                 "shading": (cnt["rays"] / (64 * cnt["shade_rounds"])) if cnt.get("shade_rounds")
+                                 else None} if counters_ok else None,
             # wave-clock split of the counting replay (regenerating / streaming megakernels)
             "phase_split": {"traversal": cnt["trace_cycles"] / (cnt["trace_cycles"] + cnt["shade_cycles"]),
                             "shading": cnt["shade_cycles"] / (cnt["trace_cycles"] + cnt["shade_cycles"])}

@@ -59,6 +59,7 @@ public static class HalogenNative
         public ulong trace_cycles;
         public ulong shade_cycles;
         [MarshalAs(UnmanagedType.ByValArray, SizeConst = 4)] public ulong[] shade_detail;
+        public ulong shade_rounds;
     }
 
     public const int HG_OK = 0;

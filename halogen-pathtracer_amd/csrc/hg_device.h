@@ -122,6 +122,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 // ---------------------------------------------------------------------------------------------------
 struct Counters {
     uint32_t rays, tri, aabb, node_rounds, tri_rounds, hits;  // *_rounds: wave-level loop iterations (one lane counts)
+    uint32_t shade_rounds;
 };
 // 1 in exactly one active lane (the lowest): summed over lanes, counts the wave-level executions of a code point
 // Wave clock (s_memtime) for the counting instantiations' phase split; volatile + memory clobber keep the
@@ -341,16 +342,28 @@ struct Stack {
     uint32_t lds_stride;
     uint32_t* spill;  // this lane's spill column
     uint32_t spill_stride;
-    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
-        if (__builtin_expect(sp < kLds, 1)) hg_lds_stack[__umul24(sp, lds_stride) + lane] = v;  // full-rate mad24
-        else spill[(sp - kLds) * spill_stride] = v;
-        ++sp;
+    __device__ __forceinline__ void store(uint32_t slot, uint32_t v) const {
+        if (__builtin_expect(slot < kLds, 1)) hg_lds_stack[__umul24(slot, lds_stride) + lane] = v;  // full-rate mad24
+        else spill[(slot - kLds) * spill_stride] = v;
     }
-    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const {
-        --sp;
-        if (__builtin_expect(sp < kLds, 1)) return hg_lds_stack[__umul24(sp, lds_stride) + lane];
-        uint32_t v = spill[(sp - kLds) * spill_stride];
+    __device__ __forceinline__ uint32_t load(uint32_t slot) const {
+        if (__builtin_expect(slot < kLds, 1)) return hg_lds_stack[__umul24(slot, lds_stride) + lane];
+        uint32_t v = spill[(slot - kLds) * spill_stride];
         asm volatile("" : "+v"(v));  // keeps the two loads apart (merged, they become one flat load)
+        return v;
+    }
+    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const { store(sp++, v); }
+    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const { return load(--sp); }
+    // Register-cached top (HG_STACK_TOP): entry sp-1 lives in `top`, entry k < sp-1 in slot k+1 (slot 0 takes the
+    // undefined initial top), so a pop returns at once and the slot read that refills `top` is only waited for
+    // at the next pop.  Same capacity as push/pop.
+    __device__ __forceinline__ void push_c(uint32_t& sp, uint32_t& top, uint32_t v) const {
+        store(sp++, top);
+        top = v;
+    }
+    __device__ __forceinline__ uint32_t pop_c(uint32_t& sp, uint32_t& top) const {
+        const uint32_t v = top;
+        top = load(--sp);
         return v;
     }
 };
@@ -608,12 +621,30 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
 // per-lane mesh cursor / while-while traversal as intersect(), with its state in a struct so a lane can stop
 // between steps (other lanes shade) and resume.  Same visit order, same counters, same result.
 // ---------------------------------------------------------------------------------------------------
+#if HG_NODE_PREFETCH
+// Prefetch the 128-B line holding the children's records (DFS pair layout: siblings share a line) while the
+// current record's boxes are tested: a 4-B load straight into a per-wave LDS sink (no VGPR is written), whose only
+// purpose is to pull the line into the caches before the next round asks for it.
+__shared__ uint32_t hg_prefetch_sink[64];
+__device__ __forceinline__ void node_prefetch(const HgKernelParams& kp, uint32_t refA, uint32_t refB) {
+    const uint32_t pf = !(refA & HG_LEAF_BIT) ? refA : refB;
+    if (!(pf & HG_LEAF_BIT))
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(uintptr_t)(reinterpret_cast<const char*>(kp.nodes) +
+                                                                       (size_t(pf) << 6)),
+            (__attribute__((address_space(3))) void*)hg_prefetch_sink, 4, 0, 0);
+}
+#endif
+
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
     uint32_t best_tri;     // triangle | orientation<0 << 31, HG_NONE: no mesh hit yet
     uint32_t best_mesh, sph, node, sp, mi;  // mi == n_meshes: traversal finished
     uint64_t live;         // exact-cull mask of the meshes
+#if HG_STACK_TOP
+    uint32_t top;  // the stack's top entry (Stack::push_c / pop_c)
+#endif
 };
 
 __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c) {
@@ -660,6 +691,9 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     // 1/ld (the same rcp_exact values mesh_local_ray computes) is not kept in Trav: live only during this round, it
     // stays out of the registers held across the streaming kernel's shading code
     const f3 inv = mk(rcp_exact(t.ld.x), rcp_exact(t.ld.y), rcp_exact(t.ld.z));
+#if HG_PHASE_DETAIL == 3
+    uint64_t tp = kp.counters ? wave_clock() : 0;
+#endif
     for (;;) {  // relaxed while-while, as in isect_meshes
         const uint32_t n_desc = uint32_t(__popcll(__ballot(act && !(t.node & HG_LEAF_BIT))));
         if (n_desc == 0u) break;
@@ -669,18 +703,32 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             const uint32_t ro = t.node << 6;
             const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
                          b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
+            const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+#if HG_NODE_PREFETCH
+            // after all four loads have landed (vmcnt retires in order: a wait for a later load would include it)
+            asm volatile("" : : "v"(a_lo.w), "v"(a_hi.w), "v"(b_lo.z), "v"(b_hi.z));
+            node_prefetch(kp, refA, refB);
+#endif
             const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), t.lo, inv);
             const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), t.lo, inv);
             c.aabb += 2;
-            const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
             const bool bFirst = dB < dA;  // :430-444
             const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
             const bool nearOk = (bFirst ? dB : dA) < t.best_t, farOk = (bFirst ? dA : dB) < t.best_t;
+#if HG_STACK_TOP
+            if (nearOk && farOk) stk.push_c(t.sp, t.top, farRef);
+            t.node = nearOk ? nearRef : farRef;
+            if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop_c(t.sp, t.top) : HG_NONE;
+#else
             if (nearOk && farOk) stk.push(t.sp, farRef);
             t.node = nearOk ? nearRef : farRef;
             if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+#endif
         }
     }
+#if HG_PHASE_DETAIL == 3
+    if (kp.counters) tp = phase_mark(kp, 11, tp);
+#endif
     if (act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
@@ -699,14 +747,29 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
                 t.best_mesh = t.mi;
             }
         }
-        t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+        t.node = t.sp > 0 ?
+#if HG_STACK_TOP
+                 stk.pop_c(t.sp, t.top)
+#else
+                 stk.pop(t.sp)
+#endif
+                 : HG_NONE;
     }
+#if HG_PHASE_DETAIL == 3
+    if (kp.counters) tp = phase_mark(kp, 12, tp);
+#endif
     if (act && t.node == HG_NONE) {
         const uint32_t nm = uint32_t(kp.n_meshes);
         t.mi = next_live_mesh(t.live, t.mi + 1u, nm);
         f3 inv_next;
         if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv_next, t.node);
     }
+#if HG_PHASE_DETAIL == 3
+    if (kp.counters) {
+        asm volatile("" : : "v"(t.node), "v"(t.lo.x), "v"(t.ld.x));
+        tp = phase_mark(kp, 13, tp);
+    }
+#endif
 }
 
 // The hit get_ray_intersection returns, from a finished traversal (:452-471 and the sphere pass).
@@ -872,8 +935,10 @@ __device__ f3 material_brdf(const HgKernelParams& kp, const Sampler& smp, Ray& r
     smp.get2(ID_PROPERTY, pr0, pr1);
     // get_random_unit_vector (HalogenRandom.hlsl:282-298)
     const float theta = rr0 * 2.0f * HLSL_PI;
-    const float phi = hg_acosf(2.0f * rr1 - 1.0f);
-    const float sT = hg_sinf(theta), cT = hg_cosf(theta), sP = hg_sinf(phi), cP = hg_cosf(phi);
+    const float phi = hg_acosf_fused(2.0f * rr1 - 1.0f);  // = hg_acosf (tests/test_fmath.py, every input)
+    float sT, cT, sP, cP;  // = hg_sinf / hg_cosf of each angle, one reduction per angle (tests/test_fmath.py)
+    hg_sincosf(theta, &sT, &cT);
+    hg_sincosf(phi, &sP, &cP);
     const f3 rv = mk(1.0f * sP * cT, 1.0f * sP * sT, 1.0f * cP);
     const float rough2 = mt.prio_id_r2.z;
     if (!(pr0 > mt.albedo.w)) {
@@ -1032,7 +1097,9 @@ __device__ Ray camera_ray(const HgKernelParams& kp, const Sampler& smp, float nd
     float fd0, fd1, j0, j1;
     smp.get2(ID_FOCAL, fd0, fd1);
     const float th = (fd0 * 360.0f) * HG_DEG2RAD;
-    const f3 ap = mk(hg_cosf(th) * kp.focal_disc_radius * fd1, hg_sinf(th) * kp.focal_disc_radius * fd1, 0.0f);
+    float sth, cth;
+    hg_sincosf(th, &sth, &cth);
+    const f3 ap = mk(cth * kp.focal_disc_radius * fd1, sth * kp.focal_disc_radius * fd1, 0.0f);
     f3 screen = mk(ndcx * kp.vw, ndcy * kp.vh, 1.0f * kp.near_);
     smp.get2(ID_JITTER, j0, j1);
     const float jx = (inv_blackman_harris(j0) - 0.5f) * 2.0f * kp.filter_radius * kp.psx;

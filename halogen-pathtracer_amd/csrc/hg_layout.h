@@ -81,6 +81,12 @@
 #ifndef HG_TRI_PREFETCH
 #define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
 #endif
+#ifndef HG_STACK_TOP
+#define HG_STACK_TOP 0  // streaming traversal: keep the stack's top entry in a register (pops off the LDS latency)
+#endif
+#ifndef HG_NODE_PREFETCH
+#define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
+#endif
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
 #endif

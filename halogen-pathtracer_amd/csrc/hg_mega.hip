@@ -144,6 +144,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         if (work) {
             const Hit hit = intersect(kp, ray, c, stk);
             if (kCounters) t1 = wave_clock();
+            c.shade_rounds += wave_once();
             bool alive = false;
             f3 thr = s_thr.get(), col = s_col.get();
             if (hit.t < kp.far_) {  // :898-936
@@ -239,6 +240,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
             atomicAdd(kp.counters + 9, (unsigned long long)cyc_trav);
             atomicAdd(kp.counters + 10, (unsigned long long)cyc_shade);
         }
+        const uint32_t sr = wave_sum(c.shade_rounds);
+        if (lane == 0 && sr) atomicAdd(kp.counters + 15, (unsigned long long)sr);
     }
 }
 
@@ -346,6 +349,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         }
         // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
         while (work && tv.mi >= nm) {
+            c.shade_rounds += wave_once();
 #if HG_PHASE_DETAIL == 1
             uint64_t tp = kCounters ? wave_clock() : 0;
 #endif
@@ -453,6 +457,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             atomicAdd(kp.counters + 9, (unsigned long long)cyc_trav);
             atomicAdd(kp.counters + 10, (unsigned long long)cyc_shade);
         }
+        const uint32_t sr = wave_sum(c.shade_rounds);
+        if (lane == 0 && sr) atomicAdd(kp.counters + 15, (unsigned long long)sr);
     }
 }
 

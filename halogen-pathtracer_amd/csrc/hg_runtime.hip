@@ -907,6 +907,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->trace_cycles = v[9];
     out->shade_cycles = v[10];
     for (int k = 0; k < 4; ++k) out->shade_detail[k] = v[11 + k];
+    out->shade_rounds = v[15];
     return HG_OK;
 }
 

@@ -152,6 +152,8 @@ typedef struct hg_counters {
     uint64_t shade_cycles; /* ... and in the rest of the bounce (shading, sampling, ray generation, accumulation) */
     uint64_t shade_detail[4]; /* analysis builds (HG_PHASE_DETAIL=1) only, streaming kernel: wave clock cycles of
                                  hit resolve / material + BSDF / path end + camera ray / next-ray setup; else 0 */
+    uint64_t shade_rounds; /* regenerating / streaming megakernels: wave-level iterations of the shading code (SIMD
+                              utilisation of shading = rays / (64 * shade_rounds)) */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;

@@ -150,6 +150,32 @@ HG_FN float hg_cosf(float x) {
 
 HG_FN float hg_tanf(float x) { return hg_sinf(x) / hg_cosf(x); }
 
+/* sin and cos of one argument with one reduction and one evaluation of each polynomial: bit-identical to
+ * (hg_sinf(x), hg_cosf(x)) for every x (the same operations on the same values; tests/test_fmath.py checks it).
+ * The separate forms stay the specification; this is what the device kernels call. */
+HG_FN void hg_sincosf(float x, float* s, float* c) {
+    float ax = x < 0.0f ? -x : x, r, z, pc, ps;
+    int j, flip, ssin, scos;
+    if (x != x) { *s = x; *c = x; return; }
+    if (ax == HG_INF) { *s = ax - ax; *c = ax - ax; return; }
+    r = hg_reduce_quadrant_(ax, &j); /* j in {0,2,4,6} */
+    flip = j > 3;
+    if (flip) j -= 4;                /* j in {0,2} */
+    z = r * r;
+    pc = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
+    pc = pc - 0.5f * z;
+    pc = pc + 1.0f;
+    ps = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r;
+    ps = ps + r;
+    ssin = (x < 0.0f) != flip;        /* hg_sinf: sign from x, flipped when j > 3 */
+    scos = flip != (j > 1);           /* hg_cosf: flipped when j > 3, and again when j > 1 */
+    {
+        const float vs = j == 2 ? pc : ps, vc = j == 0 ? pc : ps;
+        *s = ssin ? -vs : vs;
+        *c = scos ? -vc : vc;
+    }
+}
+
 /* ---- asin / acos (Cephes asinf.c / acosf.c) ---- */
 #define HG_PIO2F 1.5707963267948966192f
 
@@ -185,6 +211,32 @@ HG_FN float hg_acosf(float x) {
     if (x < -0.5f) return HG_PI - 2.0f * hg_asinf(__builtin_sqrtf(0.5f * (1.0f + x)));
     if (x > 0.5f) return 2.0f * hg_asinf(__builtin_sqrtf(0.5f * (1.0f - x)));
     return HG_PIO2F - hg_asinf(x);
+}
+
+/* hg_acosf with its three branches sharing one asin evaluation: bit-identical to hg_acosf for every x (each
+ * branch's asin argument has |a| <= 0.5 or is NaN, so asin's a > 0.5 path is never taken; tests/test_fmath.py
+ * checks every float in [-1, 1]).  Device kernels call this; hg_acosf stays the specification. */
+HG_FN float hg_acosf_fused(float x) {
+    float a, z, r;
+    int lo = x < -0.5f, hi = x > 0.5f;
+    if (x != x) return x;
+    r = lo ? __builtin_sqrtf(0.5f * (1.0f + x)) : hi ? __builtin_sqrtf(0.5f * (1.0f - x)) : x; /* asin argument */
+    /* hg_asinf(r) for |r| <= 0.5 (r >= 0 in the lo / hi branches) */
+    if (r != r) {
+        z = r;
+    } else {
+        a = r < 0.0f ? -r : r;
+        if (a < 1.0e-4f) {
+            z = a;
+        } else {
+            z = a * a;
+            z = ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+                 1.6666752422e-1f) * z * a;
+            z = z + a;
+        }
+        z = r < 0.0f ? -z : z;
+    }
+    return lo ? HG_PI - 2.0f * z : hi ? 2.0f * z : HG_PIO2F - z;
 }
 
 /* ---- log (Cephes logf.c) ---- */

@@ -1026,8 +1026,32 @@ int64_t hgo_build_blas(const float* V, int32_t n_vertices, int32_t* idx, int32_t
     return ret;
 }
 
+/* Exported for tests/test_fmath.py: the number of floats with bit patterns in [lo, hi] on which a fused device
+ * form differs (bitwise) from its specification: fn 0 hg_sincosf vs hg_sinf/hg_cosf, 1 hg_acosf_fused vs hg_acosf */
+int64_t hgo_fused_mismatches(int32_t fn, uint32_t lo, uint32_t hi) {
+    int64_t bad = 0;
+    for (uint64_t u = lo; u <= hi; u++) {
+        float v, a, b, s, c;
+        uint32_t ui = (uint32_t)u, ua, ub;
+        memcpy(&v, &ui, 4);
+        if (fn == 0) {
+            hg_sincosf(v, &s, &c);
+            a = hg_sinf(v); b = hg_cosf(v);
+            memcpy(&ua, &s, 4); memcpy(&ub, &a, 4);
+            if (ua != ub) { bad++; continue; }
+            memcpy(&ua, &c, 4); memcpy(&ub, &b, 4);
+            if (ua != ub) bad++;
+        } else {
+            a = hg_acosf_fused(v); b = hg_acosf(v);
+            memcpy(&ua, &a, 4); memcpy(&ub, &b, 4);
+            if (ua != ub) bad++;
+        }
+    }
+    return bad;
+}
+
 /* Exported for tests/test_fmath.py: evaluates the shared arithmetic spec (include/hg_fmath.h) on the host.
- * fn: 0 sin, 1 cos, 2 acos, 3 tan, 4 log, 5 exp, 6 round, 7 rnorm, 8 asin */
+ * fn: 0 sin, 1 cos, 2 acos, 3 tan, 4 log, 5 exp, 6 round, 7 rnorm, 8 asin, 9/10 sin/cos of hg_sincosf */
 void hgo_fmath(int32_t fn, const float* x, float* y, int64_t n) {
     for (int64_t i = 0; i < n; i++) {
         float v = x[i], r;
@@ -1040,6 +1064,9 @@ void hgo_fmath(int32_t fn, const float* x, float* y, int64_t n) {
             case 5: r = hg_expf(v); break;
             case 6: r = hg_roundf(v); break;
             case 7: r = hg_rnorm(v); break;
+            case 9: { float c; hg_sincosf(v, &r, &c); break; }
+            case 10: { float sn; hg_sincosf(v, &sn, &r); break; }
+            case 11: r = hg_acosf_fused(v); break;
             default: r = hg_asinf(v); break;
         }
         y[i] = r;
