@@ -63,6 +63,9 @@
 #ifndef HG_DESCENT_T
 #define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
 #endif
+#ifndef HG_STREAM_RESHADE
+#define HG_STREAM_RESHADE 16  // streaming kernel: repeat the shading pass while at least this many lanes need it
+#endif
 #ifndef HG_STREAM_DESCENT_T
 #define HG_STREAM_DESCENT_T 6  // the same for the streaming kernel (tools/sweep42.txt)
 #endif

@@ -348,7 +348,12 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             cyc_shade -= t;
         }
         // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
-        while (work && tv.mi >= nm) {
+        // (rays that finish at once — everything culled — shade again in this loop while at least
+        // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
+        for (uint32_t it = 0;; ++it) {
+            const uint32_t n_sh = uint32_t(__popcll(__ballot(work && tv.mi >= nm)));
+            if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
+            if (!(work && tv.mi >= nm)) continue;
             c.shade_rounds += wave_once();
 #if HG_PHASE_DETAIL == 1
             uint64_t tp = kCounters ? wave_clock() : 0;
