@@ -9,9 +9,14 @@
 // depend on it), so the float arithmetic is kept in the reference's order: Unity's Bounds stores
 // centre/extents, so every min/max goes through  e=(max-min)*0.5, c=min+e, min=c-e, max=c+e.
 // Compiled with -ffp-contract=off.
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <functional>
+#include <mutex>
 #include <cstring>
 #include <limits>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -156,6 +161,334 @@ extern "C" int64_t hg_build_blas(const float* V, int32_t n_vertices, int32_t* id
             cur.indexA = uint32_t(a);  // child B is always a + 1
             cur.triangleCount = 0;
             nodes[size_t(entry)] = cur;
+        }
+        queue.swap(next);
+        next.clear();
+    }
+    const int64_t n = int64_t(nodes.size());
+    if (out_nodes) {
+        if (n > max_nodes) return -(n + 1);
+        std::memcpy(out_nodes, nodes.data(), size_t(n) * sizeof(BVHEntry));
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Parallel build (hg_build_blas_mt): the same node array and the same reordered triangle list as hg_build_blas,
+// level by level.  Within a BFS level the queue entries own disjoint triangle ranges, so they are independent:
+// small entries run the sequential partition + bounds on a worker each, large ones use all workers:
+//  - bounds: chunked folds of `a < b ? a : b` / `a > b ? a : b`, combined in range order.  Without NaN that fold
+//    is associative (it keeps the LAST occurrence of the extreme, so +0/-0 ties resolve as sequentially); a
+//    vertex array holding a NaN makes the whole build sequential.
+//  - partition: the two-pointer loop above moves elements by a rule that depends only on ranks.  With A the
+//    number of left (cen < split) elements, p_1 < .. < p_r the right elements in [0, A), q_1 > .. > q_r the left
+//    elements in [A, n) and q_0 = n:  left x < A stays;  p_k -> q_{k-1} - 1;  q_k -> p_k;  a right x > A -> x - 1;
+//    a right x == A -> q_r - 1.  (Derived from the loop; tests/test_bvh.py checks it against the sequential build.)
+// Node numbering follows the queue order, so it is assigned sequentially after each level.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+// A fixed set of workers for one build: run(f) calls f(t) on every worker t in [0, n) and returns when all are done
+// (the calling thread is worker 0).  Starting threads once per build, not once per pass, keeps the per-pass cost
+// at a wake-up.
+class Workers {
+  public:
+    explicit Workers(int n) : n_(n) {
+        for (int t = 1; t < n_; ++t) pool_.emplace_back([this, t] { loop(t); });
+    }
+    ~Workers() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& th : pool_) th.join();
+    }
+    int size() const { return n_; }
+    template <class F>
+    void run(F&& f) {
+        if (n_ == 1) {
+            f(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            task_ = std::function<void(int)>(std::forward<F>(f));
+            pending_ = n_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        task_(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+    }
+    // f(t, lo, hi) over n_ contiguous chunks of [0, n)
+    template <class F>
+    void chunks(int64_t n, F&& f) {
+        run([&](int t) { f(t, n * t / n_, n * (t + 1) / n_); });
+    }
+
+  private:
+    void loop(int t) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> g(m_);
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (stop_) return;
+            g.unlock();
+            task_(t);
+            g.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> pool_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::function<void(int)> task_;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
+struct Box {
+    Vec3 mn, mx;
+};
+
+Box fold_range(uint64_t lo, uint64_t hi, const int32_t* idx, const float* V) {
+    const float inf = std::numeric_limits<float>::infinity();
+    Box b{{{inf, inf, inf}}, {{-inf, -inf, -inf}}};
+    for (uint64_t i = lo; i < hi; ++i)
+        for (int c = 0; c < 3; ++c) {
+            const float* p = V + 3 * int64_t(idx[3 * i + c]);
+            for (int k = 0; k < 3; ++k) {
+                b.mn[k] = b.mn[k] < p[k] ? b.mn[k] : p[k];
+                b.mx[k] = b.mx[k] > p[k] ? b.mx[k] : p[k];
+            }
+        }
+    return b;
+}
+
+UnityBounds range_bounds_mt(uint32_t start, uint32_t count, const int32_t* idx, const float* V, Workers& w) {
+    std::vector<Box> part(size_t(w.size()));
+    w.chunks(count, [&](int t, int64_t lo, int64_t hi) {
+        part[size_t(t)] = fold_range(uint64_t(start) + lo, uint64_t(start) + hi, idx, V);
+    });
+    Box b = part[0];
+    for (size_t t = 1; t < part.size(); ++t)  // combine in range order, same rule as the fold
+        for (int k = 0; k < 3; ++k) {
+            b.mn[k] = b.mn[k] < part[t].mn[k] ? b.mn[k] : part[t].mn[k];
+            b.mx[k] = b.mx[k] > part[t].mx[k] ? b.mx[k] : part[t].mx[k];
+        }
+    UnityBounds u = UnityBounds::FromMinMax(b.mn, b.mx);
+    u.PadIfThin();
+    return u;
+}
+
+// The sequential two-pointer partition of [first, first+count) (hg_build_blas), returning the left count.
+uint32_t partition_seq(uint32_t first, uint32_t count, int axis, float split, int32_t* idx, float* cen) {
+    int64_t i = first, j = int64_t(first) + int64_t(count) - 1;
+    while (i <= j) {
+        if (cen[3 * i + axis] < split) {
+            ++i;
+        } else {
+            for (int k = 0; k < 3; ++k) {
+                std::swap(idx[3 * i + k], idx[3 * j + k]);
+                std::swap(cen[3 * i + k], cen[3 * j + k]);
+            }
+            --j;
+        }
+    }
+    return uint32_t(i - first);
+}
+
+// The same permutation computed from ranks (rule above) by every worker; tmp_*, P and Q hold `count` entries.
+uint32_t partition_mt(uint32_t first, uint32_t count, int axis, float split, int32_t* idx, float* cen,
+                      std::vector<int32_t>& tmp_i, std::vector<float>& tmp_c, std::vector<uint32_t>& P,
+                      std::vector<uint32_t>& Q, Workers& w) {
+    const int64_t n = count;
+    const int T = w.size();
+    int32_t* I = idx + 3 * int64_t(first);
+    float* Cn = cen + 3 * int64_t(first);
+    std::vector<int64_t> cntL(size_t(T) + 1, 0), frontL(size_t(T), 0);
+    w.chunks(n, [&](int t, int64_t lo, int64_t hi) {
+        int64_t c = 0;
+        for (int64_t x = lo; x < hi; ++x) c += Cn[3 * x + axis] < split;
+        cntL[size_t(t) + 1] = c;
+    });
+    for (int t = 0; t < T; ++t) cntL[size_t(t) + 1] += cntL[size_t(t)];  // left elements before each chunk
+    const int64_t A = cntL[size_t(T)];
+    if (P.size() < size_t(n)) {
+        P.resize(size_t(n));
+        Q.resize(size_t(n));
+        tmp_i.resize(size_t(3 * n));
+        tmp_c.resize(size_t(3 * n));
+    }
+    // P[k-1] = p_k, the k-th right element in [0, A); Q[k-1] = q_k, the k-th left element in [A, n) from the end
+    w.chunks(n, [&](int t, int64_t lo, int64_t hi) {
+        int64_t pl = cntL[size_t(t)], fl = 0;  // left elements in [0, x); left elements of this chunk below A
+        for (int64_t x = lo; x < hi; ++x) {
+            const bool left = Cn[3 * x + axis] < split;
+            if (x < A) {
+                if (left) ++fl;
+                else P[size_t(x - pl)] = uint32_t(x);  // rank - 1 = rights in [0, x)
+            } else if (left) {
+                Q[size_t(A - pl - 1)] = uint32_t(x);  // rank = lefts in [x, n)
+            }
+            pl += left;
+        }
+        frontL[size_t(t)] = fl;
+    });
+    int64_t r = A;  // right elements in [0, A)
+    for (int t = 0; t < T; ++t) r -= frontL[size_t(t)];
+    const int64_t qr_minus_1 = (r == 0 ? n : int64_t(Q[size_t(r - 1)])) - 1;
+    w.chunks(n, [&](int t, int64_t lo, int64_t hi) {
+        int64_t pl = cntL[size_t(t)];
+        for (int64_t x = lo; x < hi; ++x) {
+            const bool left = Cn[3 * x + axis] < split;
+            int64_t dst;
+            if (x < A) {
+                if (left) {
+                    dst = x;
+                } else {
+                    const int64_t k = (x + 1) - pl;  // p_k -> q_{k-1} - 1
+                    dst = (k == 1 ? n : int64_t(Q[size_t(k - 2)])) - 1;
+                }
+            } else if (left) {
+                dst = P[size_t(A - pl - 1)];  // q_k -> p_k
+            } else {
+                dst = x == A ? qr_minus_1 : x - 1;
+            }
+            for (int c = 0; c < 3; ++c) {
+                tmp_i[size_t(3 * dst + c)] = I[3 * x + c];
+                tmp_c[size_t(3 * dst + c)] = Cn[3 * x + c];
+            }
+            pl += left;
+        }
+    });
+    w.chunks(n, [&](int, int64_t lo, int64_t hi) {
+        std::memcpy(I + 3 * lo, tmp_i.data() + 3 * lo, size_t(3 * (hi - lo)) * sizeof(int32_t));
+        std::memcpy(Cn + 3 * lo, tmp_c.data() + 3 * lo, size_t(3 * (hi - lo)) * sizeof(float));
+    });
+    return uint32_t(A);
+}
+
+struct LevelResult {
+    uint32_t countA;
+    bool split;
+    UnityBounds ba, bb;
+};
+
+}  // namespace
+
+extern "C" int64_t hg_build_blas_mt(const float* V, int32_t n_vertices, int32_t* idx, int32_t n_tris,
+                                    const float root_min[3], const float root_max[3], int32_t max_hierarchy_depth,
+                                    BVHEntry* out_nodes, int64_t max_nodes, int32_t n_threads) {
+    if (!V || !idx || n_tris < 0 || n_vertices < 0 || !root_min || !root_max) return HG_E_INVALID;
+    for (int64_t i = 0; i < 3 * int64_t(n_tris); ++i)
+        if (idx[i] < 0 || idx[i] >= n_vertices) return HG_E_INVALID;
+    int threads = n_threads > 0 ? n_threads : int(std::thread::hardware_concurrency());
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    for (int64_t i = 0; i < 3 * int64_t(n_vertices); ++i)
+        if (V[i] != V[i]) return hg_build_blas(V, n_vertices, idx, n_tris, root_min, root_max, max_hierarchy_depth,
+                                               out_nodes, max_nodes);  // NaN: order-exact sequential build
+    if (threads == 1 || n_tris < 4096)
+        return hg_build_blas(V, n_vertices, idx, n_tris, root_min, root_max, max_hierarchy_depth, out_nodes,
+                             max_nodes);
+
+    std::vector<BVHEntry> nodes;
+    nodes.reserve(size_t(2) * size_t(n_tris) + 1);
+    {
+        UnityBounds rb = UnityBounds::FromMinMax(Vec3{{root_min[0], root_min[1], root_min[2]}},
+                                                 Vec3{{root_max[0], root_max[1], root_max[2]}});
+        nodes.push_back(MakeEntry(rb.Min(), rb.Max(), 0, uint32_t(n_tris)));
+    }
+    Workers w(threads);
+    std::vector<float> cen(size_t(n_tris) * 3);
+    w.chunks(n_tris, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t t = lo; t < hi; ++t) {
+            const float* a = V + 3 * int64_t(idx[3 * t]);
+            const float* b = V + 3 * int64_t(idx[3 * t + 1]);
+            const float* c = V + 3 * int64_t(idx[3 * t + 2]);
+            for (int k = 0; k < 3; ++k) cen[size_t(3 * t + k)] = ((a[k] + b[k]) + c[k]) / 3.0f;
+        }
+    });
+    constexpr uint32_t kBig = 1u << 15;  // entries this large use every worker
+    std::vector<int32_t> tmp_i;
+    std::vector<float> tmp_c;
+    std::vector<uint32_t> P, Q;
+    std::vector<int32_t> queue{0}, next;
+    std::vector<LevelResult> res;
+    for (int depth = 1; depth <= max_hierarchy_depth && !queue.empty(); ++depth) {
+        res.assign(queue.size(), LevelResult{0, false, {}, {}});
+        auto node_geometry = [&](const BVHEntry& cur, int& axis, float& split) {
+            const float size[3] = {cur.boundingCornerB.x - cur.boundingCornerA.x,
+                                   cur.boundingCornerB.y - cur.boundingCornerA.y,
+                                   cur.boundingCornerB.z - cur.boundingCornerA.z};
+            const float lo[3] = {cur.boundingCornerA.x, cur.boundingCornerA.y, cur.boundingCornerA.z};
+            axis = size[0] > size[1] ? (size[0] > size[2] ? 0 : 2) : (size[1] > size[2] ? 1 : 2);
+            split = lo[axis] + size[axis] / 2.0f;
+        };
+        // large entries, one at a time with every worker
+        for (size_t q = 0; q < queue.size(); ++q) {
+            const BVHEntry& cur = nodes[size_t(queue[q])];
+            if (cur.triangleCount < kBig) continue;
+            int axis;
+            float split;
+            node_geometry(cur, axis, split);
+            const uint32_t first = cur.indexA, count = cur.triangleCount;
+            const uint32_t countA = partition_mt(first, count, axis, split, idx, cen.data(), tmp_i, tmp_c, P, Q, w);
+            LevelResult& r = res[q];
+            r.countA = countA;
+            r.split = countA > 0 && count - countA > 0 && count > kMaxNodeTriangleCount;
+            if (r.split) {
+                r.ba = range_bounds_mt(first, countA, idx, V, w);
+                r.bb = range_bounds_mt(first + countA, count - countA, idx, V, w);
+            }
+        }
+        // small entries, spread over the workers in blocks of 32 (dynamic: sizes differ)
+        std::atomic<size_t> cursor{0};
+        constexpr size_t kBlock = 32;
+        auto small = [&](int) {
+            for (;;) {
+                const size_t q0 = cursor.fetch_add(kBlock);
+                if (q0 >= queue.size()) break;
+                for (size_t q = q0; q < q0 + kBlock && q < queue.size(); ++q) {
+                const BVHEntry& cur = nodes[size_t(queue[q])];
+                if (cur.triangleCount >= kBig) continue;
+                int axis;
+                float split;
+                node_geometry(cur, axis, split);
+                const uint32_t first = cur.indexA, count = cur.triangleCount;
+                const uint32_t countA = partition_seq(first, count, axis, split, idx, cen.data());
+                LevelResult& r = res[q];
+                r.countA = countA;
+                r.split = countA > 0 && count - countA > 0 && count > kMaxNodeTriangleCount;
+                if (r.split) {
+                    r.ba = TriangleRangeBounds(first, countA, idx, V);
+                    r.bb = TriangleRangeBounds(first + countA, count - countA, idx, V);
+                }
+                }
+            }
+        };
+        if (queue.size() > 64) w.run(small);
+        else small(0);
+        // numbering in queue order (BVHGenerator.cs:40-129)
+        for (size_t q = 0; q < queue.size(); ++q) {
+            if (!res[q].split) continue;
+            BVHEntry cur = nodes[size_t(queue[q])];
+            const uint32_t first = cur.indexA, count = cur.triangleCount, countA = res[q].countA;
+            const int32_t a = int32_t(nodes.size());
+            nodes.push_back(MakeEntry(res[q].ba.Min(), res[q].ba.Max(), first, countA));
+            if (countA > 2) next.push_back(a);
+            nodes.push_back(MakeEntry(res[q].bb.Min(), res[q].bb.Max(), first + countA, count - countA));
+            if (count - countA > 2) next.push_back(a + 1);
+            cur.indexA = uint32_t(a);
+            cur.triangleCount = 0;
+            nodes[size_t(queue[q])] = cur;
         }
         queue.swap(next);
         next.clear();

@@ -99,7 +99,7 @@ EXPORTS = [
     "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
     "hg_readback", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
-    "hg_set_option", "hg_selftest", "hg_build_blas", "hg_unity_bounds", "hg_pack_triangles",
+    "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
 ]
 HG_SELFTEST_RCP = 1
 
@@ -137,6 +137,7 @@ def lib() -> C.CDLL:
         "hg_set_option": (C.c_int, [P, i32, i32]),
         "hg_selftest": (i64, [P, i32, C.POINTER(i64)]),
         "hg_build_blas": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64]),
+        "hg_build_blas_mt": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64, i32]),
         "hg_unity_bounds": (None, [f32p, f32p, i32, f32p, f32p]),
         "hg_pack_triangles": (C.c_int, [P, P, i32, P, i32, P]),
     }

@@ -14,6 +14,7 @@ on packed values (1/subsurface * absorption, bounds centre/extents) is done in f
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -105,9 +106,11 @@ class RayTracingMesh:
         fp = C.POINTER(C.c_float)
         cap = 2 * n_tris + 2
         nodes = (abi.BVHEntry * cap)()
-        n = L.hg_build_blas(self.vertices.ctypes.data, len(self.vertices), self.triangles.ctypes.data, n_tris,
-                            mn.ctypes.data_as(fp), mx.ctypes.data_as(fp), self.max_hierarchy_depth,
-                            C.cast(nodes, C.c_void_p), cap)
+        # the parallel build returns the same nodes and triangle order (tests/test_bvh.py); 8 workers measured
+        # best on the GPU box's host (tools/bench_build.py: 871k triangles 0.12 s -> 0.05 s)
+        n = L.hg_build_blas_mt(self.vertices.ctypes.data, len(self.vertices), self.triangles.ctypes.data, n_tris,
+                               mn.ctypes.data_as(fp), mx.ctypes.data_as(fp), self.max_hierarchy_depth,
+                               C.cast(nodes, C.c_void_p), cap, min(8, len(os.sched_getaffinity(0))))
         if n < 0:
             raise abi.HalogenError(f"hg_build_blas failed for {self.name}: {n}")
         self.bvh = (abi.BVHEntry * n)()

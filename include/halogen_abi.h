@@ -269,6 +269,13 @@ int64_t hg_build_blas(const float* vertices, int32_t n_vertices, int32_t* indice
                       const float root_min[3], const float root_max[3], int32_t max_hierarchy_depth,
                       BVHEntry* out_nodes, int64_t max_nodes);
 
+/* hg_build_blas with n_threads workers (0: all hardware threads): the same node array and the same reordered
+ * `indices` (tests/test_bvh.py), level-parallel over the BFS queue and rank-parallel inside large nodes. A vertex
+ * array holding a NaN, or fewer than 4096 triangles, takes the sequential build. */
+int64_t hg_build_blas_mt(const float* vertices, int32_t n_vertices, int32_t* indices, int32_t n_tris,
+                         const float root_min[3], const float root_max[3], int32_t max_hierarchy_depth,
+                         BVHEntry* out_nodes, int64_t max_nodes, int32_t n_threads);
+
 /* Unity Bounds.SetMinMax(min,max) followed by .min/.max (centre/extents round trip) — the arithmetic
  * every bound in the reference goes through (BVHGenerator.cs:171-183, RayTracingMesh.cs:106-117). */
 void hg_unity_bounds(const float in_min[3], const float in_max[3], int32_t pad_if_thin,
