@@ -492,10 +492,23 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order (:404-420)
             const uint2 leaf = leaf_range(kp, node);
             const uint32_t end = leaf.x + leaf.y;
+#if HG_TRI_PREFETCH
+            float4 na = ld_off(kp.tri_a, leaf.x << 4), nb = ld_off(kp.tri_b, leaf.x << 4);
+            float nc = ld_off(kp.tri_c, leaf.x << 2);
+#endif
             for (uint32_t ti = leaf.x; ti < end; ++ti) {
                 c.tri_rounds += wave_once();
+#if HG_TRI_PREFETCH  // the next triangle's loads go out before this one is tested
+                const float4 a = na, b = nb;
+                const float cz = nc;
+                const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
+                na = ld_off(kp.tri_a, tn << 4);
+                nb = ld_off(kp.tri_b, tn << 4);
+                nc = ld_off(kp.tri_c, tn << 2);
+#else
                 const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
                 const float cz = ld_off(kp.tri_c, ti << 2);
+#endif
                 c.tri++;
                 float t, U, V;
                 bool front;
@@ -732,10 +745,23 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     if (act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
+#if HG_STREAM_TRI_PREFETCH
+        float4 na = ld_off(kp.tri_a, leaf.x << 4), nb = ld_off(kp.tri_b, leaf.x << 4);
+        float nc = ld_off(kp.tri_c, leaf.x << 2);
+#endif
         for (uint32_t ti = leaf.x; ti < end; ++ti) {
             c.tri_rounds += wave_once();
+#if HG_STREAM_TRI_PREFETCH  // the next triangle's loads go out before this one is tested
+            const float4 a = na, b = nb;
+            const float cz = nc;
+            const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
+            na = ld_off(kp.tri_a, tn << 4);
+            nb = ld_off(kp.tri_b, tn << 4);
+            nc = ld_off(kp.tri_c, tn << 2);
+#else
             const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
             const float cz = ld_off(kp.tri_c, ti << 2);
+#endif
             c.tri++;
             float tt, U, V;
             bool front;
