@@ -649,6 +649,49 @@ __device__ __forceinline__ void node_prefetch(const HgKernelParams& kp, uint32_t
 }
 #endif
 
+// ---- wave-wide inclusive scans over 64 lanes (DPP row shifts + row broadcasts, the GFX9 form); every lane of the
+// wave must be active
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_(uint32_t x) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), kCtrl, kRowMask, 0xF, false));  // invalid source: 0
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += dpp_<0x111, 0xF>(x);  // row_shr:1
+    x += dpp_<0x112, 0xF>(x);  // row_shr:2
+    x += dpp_<0x114, 0xF>(x);  // row_shr:4
+    x += dpp_<0x118, 0xF>(x);  // row_shr:8
+    x += dpp_<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+    x += dpp_<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp_<0x111, 0xF>(x));
+    x = max(x, dpp_<0x112, 0xF>(x));
+    x = max(x, dpp_<0x114, 0xF>(x));
+    x = max(x, dpp_<0x118, 0xF>(x));
+    x = max(x, dpp_<0x142, 0xA>(x));
+    x = max(x, dpp_<0x143, 0xC>(x));
+    return x;
+}
+// Lanes of one wave exchanging data through LDS: the fences make the other lanes' LDS writes visible to this lane's
+// later reads (and keep the compiler from forwarding its own stores across them).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-wave LDS scratch of the distributed leaf test (HG_LEAF_DIST): per lane, the best (t bits << 32 | triangle)
+// key found for its ray, and one word of the owner table.  3 words per lane.
+constexpr uint32_t kLeafShareWords = 3;
+struct LeafShare {
+    uint32_t w;  // word offset of this wave's 192-word region (even: the keys are u64)
+    __device__ __forceinline__ unsigned long long* key(uint32_t i) const {
+        return reinterpret_cast<unsigned long long*>(hg_lds_stack + w) + i;
+    }
+    __device__ __forceinline__ uint32_t& tab(uint32_t i) const { return hg_lds_stack[w + 128u + i]; }
+};
+
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
@@ -696,11 +739,77 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
 #endif
 }
 
+__device__ __forceinline__ float bperm_f(int addr, float x) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(x)));
+}
+
+// Distributed leaf test (HG_LEAF_DIST; HC:404-420): the triangles of every lane's current leaf form (ray, triangle)
+// pairs numbered lane by lane (a wave prefix sum of the leaf sizes), and each round all 64 lanes test 64 of them.
+// A pair's lane finds its owner through a per-wave table (the owner's lane id stored at the pair index where its
+// run starts, then a running max over the lanes), fetches the owner's local ray and best_t by ds_bpermute, and
+// folds an accepted hit into the owner's key (t bits << 32 | triangle) with an LDS 64-bit atomic min.  After each
+// round an owner whose key came from that round pulls u, v and the facing from the winning pair's lane.
+// Exact: in the reference's sequential loop every acceptance condition but `t < closest` is independent of the
+// other triangles, and `closest` only falls, so the loop ends on the first triangle (in leaf order) of minimal t
+// among those with t < best_t at the leaf's start.  t > 1e-4 is positive, so its bit pattern orders like its
+// value, and the lower triangle index wins a tie: the key minimum is that triangle.  Counters are the same
+// (one triangle test per pair).  Every lane of the wave must be active.
+__device__ __forceinline__ void leaf_dist(const HgKernelParams& kp, Trav& t, Counters& c, const LeafShare& ls,
+                                          uint32_t first, uint32_t n) {
+    const uint32_t lane = __lane_id();
+    const uint32_t incl = wave_incl_add(n);
+    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+    if (total == 0u) return;
+    const uint32_t start = incl - n;
+    const uint32_t fo = first - start;  // owner's triangle index = fo + pair index (mod 2^32)
+    if (n) *ls.key(lane) = ~0ull;
+    for (uint32_t base = 0; base < total; base += 64u) {
+        c.tri_rounds += wave_once();
+        ls.tab(lane) = 0u;
+        wave_lds_sync();
+        if (n && start < base + 64u && incl > base) ls.tab(start > base ? start - base : 0u) = lane + 1u;
+        wave_lds_sync();
+        const uint32_t o = wave_incl_max(ls.tab(lane)) - 1u;  // owner lane of pair base + lane
+        const int addr = int(o << 2);
+        const f3 olo = mk(bperm_f(addr, t.lo.x), bperm_f(addr, t.lo.y), bperm_f(addr, t.lo.z));
+        const f3 old = mk(bperm_f(addr, t.ld.x), bperm_f(addr, t.ld.y), bperm_f(addr, t.ld.z));
+        const float obt = bperm_f(addr, t.best_t);
+        const uint32_t ti = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(fo))) + base + lane;
+        bool acc = false;
+        float tt = 0.0f, U = 0.0f, V = 0.0f;
+        bool front = false;
+        if (base + lane < total) {
+            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+            const float cz = ld_off(kp.tri_c, ti << 2);
+            c.tri++;
+            acc = tri_accept(olo, old, a, b, cz, obt, tt, U, V, front);
+        }
+        wave_lds_sync();
+        if (acc) atomicMin(ls.key(o), (static_cast<unsigned long long>(__float_as_uint(tt)) << 32) | ti);
+        wave_lds_sync();
+        // owners: did this round's pairs improve the key?  Then pull u, v, facing from the winning pair's lane.
+        unsigned long long k = ~0ull;
+        if (n) k = *ls.key(lane);
+        const uint32_t wp = uint32_t(k) - fo - base;  // winning pair's lane, when it is in this round
+        const bool mine = n && k != ~0ull && wp < 64u && uint32_t(k) - fo < total;
+        const int src = int((wp & 63u) << 2);
+        const float wu = bperm_f(src, U), wv = bperm_f(src, V);
+        const uint32_t wf = uint32_t(__builtin_amdgcn_ds_bpermute(src, front ? 1 : 0));
+        if (mine) {
+            t.best_t = __uint_as_float(uint32_t(k >> 32));
+            t.best_u = wu;
+            t.best_v = wv;
+            t.best_tri = uint32_t(k) | (wf ? 0u : 0x80000000u);
+            t.best_mesh = t.mi;
+        }
+    }
+}
+
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
 // leaf, and move to the next live mesh when the current one is exhausted.
 template <class Stk>
 __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
-                                          const Stk& stk, bool act) {
+                                          const Stk& stk, bool act, const LeafShare& ls) {
     // 1/ld (the same rcp_exact values mesh_local_ray computes) is not kept in Trav: live only during this round, it
     // stays out of the registers held across the streaming kernel's shading code
     const f3 inv = mk(rcp_exact(t.ld.x), rcp_exact(t.ld.y), rcp_exact(t.ld.z));
@@ -742,7 +851,27 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
 #if HG_PHASE_DETAIL == 3
     if (kp.counters) tp = phase_mark(kp, 11, tp);
 #endif
-    if (act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
+    bool seq_leaf = true;  // the leaf's triangles tested by the lane itself, in order
+#if HG_LEAF_DIST
+    {
+        const bool at_leaf = act && t.node != HG_NONE && (t.node & HG_LEAF_BIT);
+        uint32_t first = 0u, n = 0u;
+        if (at_leaf) {
+            const uint2 lr = leaf_range(kp, t.node);
+            first = lr.x;
+            n = lr.y;
+        }
+        // distribute only when the longest leaf would take enough sequential rounds to pay for the exchange
+        if (HG_LEAF_DIST_MIN <= 1 || uint32_t(__builtin_amdgcn_readlane(int(wave_incl_max(n)), 63)) >= HG_LEAF_DIST_MIN) {
+            leaf_dist(kp, t, c, ls, first, n);
+            if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+            seq_leaf = false;
+        }
+    }
+#else
+    (void)ls;
+#endif
+    if (seq_leaf && act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
 #if HG_STREAM_TRI_PREFETCH

@@ -87,6 +87,12 @@
 #ifndef HG_STREAM_TRI_PREFETCH
 #define HG_STREAM_TRI_PREFETCH 1  // the same in the streaming kernel's leaf loop: C3 +3 % at no register cost
 #endif
+#ifndef HG_LEAF_DIST
+#define HG_LEAF_DIST 1  // streaming traversal: a round's (ray, triangle) pairs dealt over all 64 lanes, LDS min-reduce
+#endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweep52.txt)
+#ifndef HG_LEAF_DIST_MIN
+#define HG_LEAF_DIST_MIN 1  // ... only when the wave's longest leaf has at least this many triangles (1: always;
+#endif                      // 2 / 3 measured 2066 / 2063)
 #ifndef HG_STACK_TOP
 #define HG_STACK_TOP 0  // streaming traversal: keep the stack's top entry in a register (pops off the LDS latency)
 #endif

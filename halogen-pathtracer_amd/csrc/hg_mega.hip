@@ -304,6 +304,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
     const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
     const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
+    const LeafShare ls{(lds_depth + kRegenLdsState) * blockDim.x + (threadIdx.x >> 6) * (kLeafShareWords * 64u)};
     const uint32_t nm = uint32_t(kp.n_meshes);
     bool work;
     uint32_t px, py;
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             const uint32_t n_act = uint32_t(__popcll(__ballot(act)));
             if (n_act == 0) break;
             if (n_act <= HG_STREAM_TMIN && __any(work && !act)) break;
-            trav_step(kp, ray, tv, c, stk, act);
+            trav_step(kp, ray, tv, c, stk, act, ls);
         }
         if (kCounters) {
             const uint64_t t = wave_clock();
@@ -471,7 +472,8 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool count
     const int tiles_per_block = block / 64;
     const int grid = (kp.n_local_tiles * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
-    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4 +
+                       (HG_LEAF_DIST ? size_t(kLeafShareWords) * size_t(block) * 4 : 0);
     if (counters)
         hipLaunchKernelGGL(hg_trace_stream_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
     else
