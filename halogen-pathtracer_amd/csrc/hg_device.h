@@ -417,6 +417,125 @@ __device__ __forceinline__ void resolve_mesh(const HgKernelParams& kp, const Ray
     h.pos = ray.o + ray.d * best_t;
 }
 
+// ---- wave-wide inclusive scans over 64 lanes (DPP row shifts + row broadcasts, the GFX9 form); every lane of the
+// wave must be active
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_(uint32_t x) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), kCtrl, kRowMask, 0xF, false));  // invalid source: 0
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += dpp_<0x111, 0xF>(x);  // row_shr:1
+    x += dpp_<0x112, 0xF>(x);  // row_shr:2
+    x += dpp_<0x114, 0xF>(x);  // row_shr:4
+    x += dpp_<0x118, 0xF>(x);  // row_shr:8
+    x += dpp_<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+    x += dpp_<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp_<0x111, 0xF>(x));
+    x = max(x, dpp_<0x112, 0xF>(x));
+    x = max(x, dpp_<0x114, 0xF>(x));
+    x = max(x, dpp_<0x118, 0xF>(x));
+    x = max(x, dpp_<0x142, 0xA>(x));
+    x = max(x, dpp_<0x143, 0xC>(x));
+    return x;
+}
+// Lanes of one wave exchanging data through LDS: the fences make the other lanes' LDS writes visible to this lane's
+// later reads (and keep the compiler from forwarding its own stores across them).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-wave LDS scratch of the distributed leaf test (HG_LEAF_DIST): per lane, the best (t bits << 32 | triangle)
+// key found for its ray, and one word of the owner table.  3 words per lane.
+constexpr uint32_t kLeafShareWords = 3;
+struct LeafShare {
+    uint32_t w;  // word offset of this wave's 192-word region (even: the keys are u64)
+    __device__ __forceinline__ unsigned long long* key(uint32_t i) const {
+        return reinterpret_cast<unsigned long long*>(hg_lds_stack + w) + i;
+    }
+    __device__ __forceinline__ uint32_t& tab(uint32_t i) const { return hg_lds_stack[w + 128u + i]; }
+};
+
+__device__ __forceinline__ float bperm_f(int addr, float x) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(x)));
+}
+
+// Distributed leaf test (HG_LEAF_DIST; HC:404-420): the triangles of every lane's current leaf form (ray, triangle)
+// pairs numbered lane by lane (a wave prefix sum of the leaf sizes), and each round all 64 lanes test 64 of them.
+// A pair's lane finds its owner through a per-wave table (the owner's lane id stored at the pair index where its
+// run starts, then a running max over the lanes), fetches the owner's local ray and best_t by ds_bpermute, and
+// folds an accepted hit into the owner's key (t bits << 32 | triangle) with an LDS 64-bit atomic min.  After each
+// round an owner whose key came from that round pulls u, v and the facing from the winning pair's lane.
+// Exact: in the reference's sequential loop every acceptance condition but `t < closest` is independent of the
+// other triangles, and `closest` only falls, so the loop ends on the first triangle (in leaf order) of minimal t
+// among those with t < best_t at the leaf's start.  t > 1e-4 is positive, so its bit pattern orders like its
+// value, and the lower triangle index wins a tie: the key minimum is that triangle.  Counters are the same
+// (one triangle test per pair).  Every lane of the wave must be active.
+struct LeafRay {  // the lane's side of a leaf test: its mesh-local ray and running best hit
+    const f3& lo;
+    const f3& ld;
+    float& best_t;
+    float& best_u;
+    float& best_v;
+    uint32_t& best_tri;
+    uint32_t& best_mesh;
+    uint32_t mi;
+};
+__device__ __forceinline__ void leaf_dist(const HgKernelParams& kp, const LeafRay& t, Counters& c, const LeafShare& ls,
+                                          uint32_t first, uint32_t n) {
+    const uint32_t lane = __lane_id();
+    const uint32_t incl = wave_incl_add(n);
+    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+    if (total == 0u) return;
+    const uint32_t start = incl - n;
+    const uint32_t fo = first - start;  // owner's triangle index = fo + pair index (mod 2^32)
+    if (n) *ls.key(lane) = ~0ull;
+    for (uint32_t base = 0; base < total; base += 64u) {
+        c.tri_rounds += wave_once();
+        ls.tab(lane) = 0u;
+        wave_lds_sync();
+        if (n && start < base + 64u && incl > base) ls.tab(start > base ? start - base : 0u) = lane + 1u;
+        wave_lds_sync();
+        const uint32_t o = wave_incl_max(ls.tab(lane)) - 1u;  // owner lane of pair base + lane
+        const int addr = int(o << 2);
+        const f3 olo = mk(bperm_f(addr, t.lo.x), bperm_f(addr, t.lo.y), bperm_f(addr, t.lo.z));
+        const f3 old = mk(bperm_f(addr, t.ld.x), bperm_f(addr, t.ld.y), bperm_f(addr, t.ld.z));
+        const float obt = bperm_f(addr, t.best_t);
+        const uint32_t ti = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(fo))) + base + lane;
+        bool acc = false;
+        float tt = 0.0f, U = 0.0f, V = 0.0f;
+        bool front = false;
+        if (base + lane < total) {
+            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
+            const float cz = ld_off(kp.tri_c, ti << 2);
+            c.tri++;
+            acc = tri_accept(olo, old, a, b, cz, obt, tt, U, V, front);
+        }
+        wave_lds_sync();
+        if (acc) atomicMin(ls.key(o), (static_cast<unsigned long long>(__float_as_uint(tt)) << 32) | ti);
+        wave_lds_sync();
+        // owners: did this round's pairs improve the key?  Then pull u, v, facing from the winning pair's lane.
+        unsigned long long k = ~0ull;
+        if (n) k = *ls.key(lane);
+        const uint32_t wp = uint32_t(k) - fo - base;  // winning pair's lane, when it is in this round
+        const bool mine = n && k != ~0ull && wp < 64u && uint32_t(k) - fo < total;
+        const int src = int((wp & 63u) << 2);
+        const float wu = bperm_f(src, U), wv = bperm_f(src, V);
+        const uint32_t wf = uint32_t(__builtin_amdgcn_ds_bpermute(src, front ? 1 : 0));
+        if (mine) {
+            t.best_t = __uint_as_float(uint32_t(k >> 32));
+            t.best_u = wu;
+            t.best_v = wv;
+            t.best_tri = uint32_t(k) | (wf ? 0u : 0x80000000u);
+            t.best_mesh = t.mi;
+        }
+    }
+}
+
 // get_ray_scene_intersection_mesh, :378-472.
 // The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
 // the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
@@ -427,7 +546,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     float best_t = h.t;  // closestIntersection.rayT starts at the sphere hit (:381)
     float best_u = 0.0f, best_v = 0.0f;
     uint32_t best_tri = HG_NONE;  // global triangle index | (orientation < 0) << 31
-    int best_mesh = -1;
+    uint32_t best_mesh = 0;
     uint32_t culled = 0;
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     const uint64_t live = mesh_live_mask(kp, ray.o, winv, best_t, culled);
@@ -517,7 +636,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                     best_u = U;
                     best_v = V;
                     best_tri = ti | (front ? 0u : 0x80000000u);
-                    best_mesh = int(mi);
+                    best_mesh = mi;
                 }
             }
             node = sp > 0 ? stk.pop(sp) : HG_NONE;
@@ -598,7 +717,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                         best_u = U;
                         best_v = V;
                         best_tri = ti | (front ? 0u : 0x80000000u);
-                        best_mesh = mi;
+                        best_mesh = uint32_t(mi);
                     }
                 }
                 node = sp > 0 ? stk.pop(sp) : HG_NONE;
@@ -609,7 +728,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
 #endif
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
-        resolve_mesh(kp, ray, best_t, best_u, best_v, best_tri, uint32_t(best_mesh), h);
+        resolve_mesh(kp, ray, best_t, best_u, best_v, best_tri, best_mesh, h);
         return true;
     }
     return false;
@@ -648,49 +767,6 @@ __device__ __forceinline__ void node_prefetch(const HgKernelParams& kp, uint32_t
             (__attribute__((address_space(3))) void*)hg_prefetch_sink, 4, 0, 0);
 }
 #endif
-
-// ---- wave-wide inclusive scans over 64 lanes (DPP row shifts + row broadcasts, the GFX9 form); every lane of the
-// wave must be active
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ uint32_t dpp_(uint32_t x) {
-    return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), kCtrl, kRowMask, 0xF, false));  // invalid source: 0
-}
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
-    x += dpp_<0x111, 0xF>(x);  // row_shr:1
-    x += dpp_<0x112, 0xF>(x);  // row_shr:2
-    x += dpp_<0x114, 0xF>(x);  // row_shr:4
-    x += dpp_<0x118, 0xF>(x);  // row_shr:8
-    x += dpp_<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
-    x += dpp_<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    x = max(x, dpp_<0x111, 0xF>(x));
-    x = max(x, dpp_<0x112, 0xF>(x));
-    x = max(x, dpp_<0x114, 0xF>(x));
-    x = max(x, dpp_<0x118, 0xF>(x));
-    x = max(x, dpp_<0x142, 0xA>(x));
-    x = max(x, dpp_<0x143, 0xC>(x));
-    return x;
-}
-// Lanes of one wave exchanging data through LDS: the fences make the other lanes' LDS writes visible to this lane's
-// later reads (and keep the compiler from forwarding its own stores across them).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Per-wave LDS scratch of the distributed leaf test (HG_LEAF_DIST): per lane, the best (t bits << 32 | triangle)
-// key found for its ray, and one word of the owner table.  3 words per lane.
-constexpr uint32_t kLeafShareWords = 3;
-struct LeafShare {
-    uint32_t w;  // word offset of this wave's 192-word region (even: the keys are u64)
-    __device__ __forceinline__ unsigned long long* key(uint32_t i) const {
-        return reinterpret_cast<unsigned long long*>(hg_lds_stack + w) + i;
-    }
-    __device__ __forceinline__ uint32_t& tab(uint32_t i) const { return hg_lds_stack[w + 128u + i]; }
-};
 
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
@@ -737,72 +813,6 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
         tp = phase_mark(kp, 13, tp);
     }
 #endif
-}
-
-__device__ __forceinline__ float bperm_f(int addr, float x) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(x)));
-}
-
-// Distributed leaf test (HG_LEAF_DIST; HC:404-420): the triangles of every lane's current leaf form (ray, triangle)
-// pairs numbered lane by lane (a wave prefix sum of the leaf sizes), and each round all 64 lanes test 64 of them.
-// A pair's lane finds its owner through a per-wave table (the owner's lane id stored at the pair index where its
-// run starts, then a running max over the lanes), fetches the owner's local ray and best_t by ds_bpermute, and
-// folds an accepted hit into the owner's key (t bits << 32 | triangle) with an LDS 64-bit atomic min.  After each
-// round an owner whose key came from that round pulls u, v and the facing from the winning pair's lane.
-// Exact: in the reference's sequential loop every acceptance condition but `t < closest` is independent of the
-// other triangles, and `closest` only falls, so the loop ends on the first triangle (in leaf order) of minimal t
-// among those with t < best_t at the leaf's start.  t > 1e-4 is positive, so its bit pattern orders like its
-// value, and the lower triangle index wins a tie: the key minimum is that triangle.  Counters are the same
-// (one triangle test per pair).  Every lane of the wave must be active.
-__device__ __forceinline__ void leaf_dist(const HgKernelParams& kp, Trav& t, Counters& c, const LeafShare& ls,
-                                          uint32_t first, uint32_t n) {
-    const uint32_t lane = __lane_id();
-    const uint32_t incl = wave_incl_add(n);
-    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
-    if (total == 0u) return;
-    const uint32_t start = incl - n;
-    const uint32_t fo = first - start;  // owner's triangle index = fo + pair index (mod 2^32)
-    if (n) *ls.key(lane) = ~0ull;
-    for (uint32_t base = 0; base < total; base += 64u) {
-        c.tri_rounds += wave_once();
-        ls.tab(lane) = 0u;
-        wave_lds_sync();
-        if (n && start < base + 64u && incl > base) ls.tab(start > base ? start - base : 0u) = lane + 1u;
-        wave_lds_sync();
-        const uint32_t o = wave_incl_max(ls.tab(lane)) - 1u;  // owner lane of pair base + lane
-        const int addr = int(o << 2);
-        const f3 olo = mk(bperm_f(addr, t.lo.x), bperm_f(addr, t.lo.y), bperm_f(addr, t.lo.z));
-        const f3 old = mk(bperm_f(addr, t.ld.x), bperm_f(addr, t.ld.y), bperm_f(addr, t.ld.z));
-        const float obt = bperm_f(addr, t.best_t);
-        const uint32_t ti = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(fo))) + base + lane;
-        bool acc = false;
-        float tt = 0.0f, U = 0.0f, V = 0.0f;
-        bool front = false;
-        if (base + lane < total) {
-            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-            const float cz = ld_off(kp.tri_c, ti << 2);
-            c.tri++;
-            acc = tri_accept(olo, old, a, b, cz, obt, tt, U, V, front);
-        }
-        wave_lds_sync();
-        if (acc) atomicMin(ls.key(o), (static_cast<unsigned long long>(__float_as_uint(tt)) << 32) | ti);
-        wave_lds_sync();
-        // owners: did this round's pairs improve the key?  Then pull u, v, facing from the winning pair's lane.
-        unsigned long long k = ~0ull;
-        if (n) k = *ls.key(lane);
-        const uint32_t wp = uint32_t(k) - fo - base;  // winning pair's lane, when it is in this round
-        const bool mine = n && k != ~0ull && wp < 64u && uint32_t(k) - fo < total;
-        const int src = int((wp & 63u) << 2);
-        const float wu = bperm_f(src, U), wv = bperm_f(src, V);
-        const uint32_t wf = uint32_t(__builtin_amdgcn_ds_bpermute(src, front ? 1 : 0));
-        if (mine) {
-            t.best_t = __uint_as_float(uint32_t(k >> 32));
-            t.best_u = wu;
-            t.best_v = wv;
-            t.best_tri = uint32_t(k) | (wf ? 0u : 0x80000000u);
-            t.best_mesh = t.mi;
-        }
-    }
 }
 
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
@@ -863,7 +873,8 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         }
         // distribute only when the longest leaf would take enough sequential rounds to pay for the exchange
         if (HG_LEAF_DIST_MIN <= 1 || uint32_t(__builtin_amdgcn_readlane(int(wave_incl_max(n)), 63)) >= HG_LEAF_DIST_MIN) {
-            leaf_dist(kp, t, c, ls, first, n);
+            leaf_dist(kp, LeafRay{t.lo, t.ld, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, t.mi}, c, ls,
+                      first, n);
             if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
             seq_leaf = false;
         }
