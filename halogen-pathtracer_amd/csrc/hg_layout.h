@@ -93,6 +93,9 @@
 #ifndef HG_LEAF_DIST_MIN
 #define HG_LEAF_DIST_MIN 1  // ... only when the wave's longest leaf has at least this many triangles (1: always;
 #endif                      // 2 / 3 measured 2066 / 2063)
+#ifndef HG_CAMERA_PASS
+#define HG_CAMERA_PASS 0  // streaming kernel, spp 1: primary rays precomputed by a coherent pass (hg_camera_rays)
+#endif
 #ifndef HG_STACK_TOP
 #define HG_STACK_TOP 0  // streaming traversal: keep the stack's top entry in a register (pops off the LDS latency)
 #endif
@@ -140,6 +143,10 @@ struct HgKernelParams {
     // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
     int32_t frame_split;
     float4* __restrict__ frame_color;
+    // camera-ray pass (spp == 1): the primary ray of every (launch frame f, slot) precomputed by hg_camera_rays,
+    // (o.xyz, d.x) in cam_a and (d.y, d.z) in cam_b at [f * n_local_tiles * 64 + slot]; null: rays made inline
+    float4* __restrict__ cam_a;
+    float2* __restrict__ cam_b;
     float4* __restrict__ pool;  // path-pool kernel: per-wave path slots (hg_pool.hip)
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;

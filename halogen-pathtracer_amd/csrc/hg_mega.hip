@@ -290,7 +290,39 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
-template <bool kCounters>
+// Camera-ray pass: the primary ray of every (frame, pixel slot) of a launch, thread per ray, so the megakernel's
+// path regeneration loads 24 B instead of running get_ray (:996-1013) under divergence.  Same function, same
+// inputs (FrameCount, pixel hash, SobolDimensionOffset 0: with spp == 1 every path starts a frame), same bits.
+__global__ __launch_bounds__(256) void hg_camera_rays(const HgKernelParams kp) {
+    const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= uint64_t(n_slots) * uint32_t(kp.n_frames)) return;
+    const uint32_t f = uint32_t(i / n_slots), slot = uint32_t(i % n_slots);
+    const int gtile = kp.rank + int(slot >> 6) * kp.n_ranks;
+    const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (slot & 7u);
+    const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + ((slot >> 3) & 7u);
+    if (px >= kp.Wu || py >= kp.Hu) return;
+    const Sampler smp{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
+    const Ray r = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);
+    kp.cam_a[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    kp.cam_b[i] = make_float2(r.d.y, r.d.z);
+}
+
+hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream) {
+    const uint64_t n = uint64_t(kp.n_local_tiles) * 64u * uint32_t(kp.n_frames);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(hg_camera_rays, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, stream, kp);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ Ray load_camera_ray(const HgKernelParams& kp, uint32_t f, uint32_t slot) {
+    const size_t i = size_t(f) * (size_t(uint32_t(kp.n_local_tiles)) * 64u) + slot;
+    const float4 a = kp.cam_a[i];
+    const float2 b = kp.cam_b[i];
+    return Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)};
+}
+
+template <bool kCounters, bool kCamPass>
 __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
@@ -325,7 +357,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     Trav tv;
     tv.mi = nm;
     if (work) {
-        ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
+        ray = kCamPass ? load_camera_ray(kp, f_begin, uint32_t(local_tile) * 64u + lane)
+                       : camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
         s_thr.set(mk(1, 1, 1));
         s_col.set(mk(0, 0, 0));
@@ -425,10 +458,14 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                 }
                 s_sum.set(sum);
                 if (next) {
-                    const int gtile = kp.rank + local_tile * kp.n_ranks;
-                    const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-                    const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-                    ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                    if (kCamPass) {  // spp == 1: `next` is always a new frame, fs >> 16
+                        ray = load_camera_ray(kp, fs >> 16, uint32_t(local_tile) * 64u + lane);
+                    } else {
+                        const int gtile = kp.rank + local_tile * kp.n_ranks;
+                        const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
+                        const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+                        ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                    }
                     thr = mk(1, 1, 1);
                     col = mk(0, 0, 0);
                     acc_rough = 0.0f;
@@ -474,10 +511,15 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool count
     if (grid == 0) return hipSuccess;
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4 +
                        (HG_LEAF_DIST ? size_t(kLeafShareWords) * size_t(block) * 4 : 0);
-    if (counters)
-        hipLaunchKernelGGL(hg_trace_stream_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
+    const bool cam = kp.cam_a != nullptr;
+    if (counters && cam)
+        hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(grid), dim3(block), lds, stream, kp);
+    else if (counters)
+        hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), dim3(grid), dim3(block), lds, stream, kp);
+    else if (cam)
+        hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), dim3(grid), dim3(block), lds, stream, kp);
     else
-        hipLaunchKernelGGL(hg_trace_stream_kernel<false>, dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), dim3(grid), dim3(block), lds, stream, kp);
     return hipGetLastError();
 }
 

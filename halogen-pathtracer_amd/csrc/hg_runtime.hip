@@ -23,6 +23,7 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
+hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream);
 hipError_t hg_launch_mega_pool(const HgKernelParams& kp, bool counters, hipStream_t stream);
 uint32_t hg_pool_slots();
 uint32_t hg_pool_tiles();
@@ -77,6 +78,7 @@ struct hg_ctx {
     DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
     DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     DevBuf pool;                 // path-pool kernel: per-wave path slots
+    DevBuf cam_a, cam_b;         // camera-ray pass: primary rays of this launch chunk
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -395,7 +397,7 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool, &c->cam_a, &c->cam_b})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -783,6 +785,22 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 return rc;
             }
         }
+        // camera-ray pass (streaming kernel, spp 1: every path starts a frame, so its primary ray depends on the
+        // pixel and FrameCount only): 24 B per (frame, slot) of a chunk, under the same cap
+        const bool cam_pass = HG_CAMERA_PASS && stream_k && kp.spp == 1 && tiles > 0;
+        if (cam_pass) {
+            const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
+            chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
+            const size_t n = size_t(tiles) * 64 * size_t(std::min(n_frames, chunk_max));
+            if (int rc = ensure(c, c->cam_a, n * sizeof(float4))) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+            if (int rc = ensure(c, c->cam_b, n * sizeof(float2))) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+        }
         const int mgrid = int((units * split + mblock / 64 - 1) / (mblock / 64));
         if (pool_k) {
             if (int rc = ensure(c, c->pool, size_t(mgrid) * hg_pool_slots() * 8 * sizeof(float4))) {
@@ -805,11 +823,15 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
             HgKernelParams kc = kp;
             kc.frame_color = static_cast<float4*>(c->frame_color.p);
+            kc.cam_a = cam_pass ? static_cast<float4*>(c->cam_a.p) : nullptr;
+            kc.cam_b = cam_pass ? static_cast<float2*>(c->cam_b.p) : nullptr;
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
-                e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
+                if (cam_pass) e = hg_launch_camera_rays(kc, c->stream);
+                if (e == hipSuccess)
+                    e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
                     : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
                                : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
                 if (e == hipSuccess && kc.frame_split > 1) e = hg_launch_blend_frames(kc, c->stream);
