@@ -80,7 +80,8 @@ def main():
                "frames_per_launch": a.frames_per_launch, "kernels": kernels}
     (out / f"{a.tag}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
     # the production kernel: the counter-free trace kernel that ran longest (the bench's timed launches)
-    prods = [k for k in kernels if k.startswith("hg_trace") and k.endswith("<false>") and kernels[k]["stats"]]
+    # (template arguments: <kCounters> or <kCounters, variant>; production = kCounters false)
+    prods = [k for k in kernels if k.startswith("hg_trace") and "<false" in k and kernels[k]["stats"]]
     PROD = max(prods, key=lambda k: kernels[k]["stats"]["calls"] * kernels[k]["stats"]["avg_ms"]) if prods else ""
     if PROD in kernels and "hbm_bytes_per_launch" in kernels[PROD]:
         t = {"tag": a.tag, "kernel": PROD, "config": a.config, "width": a.width, "height": a.height,
