@@ -48,6 +48,16 @@ def setup(name: str, first_frame: int = 1):
     return packed, params, cube, frames, accumulate
 
 
+def setup_host(name: str):
+    """The same case as the host sees it: scene, HalogenSettings and Camera (the uniforms are derived by the pass)."""
+    cfg_name, w, h, frames, accumulate, ov = CASES[name]
+    cfg = scenes.CONFIGS[cfg_name].resized(w, h, frames)
+    ov = dict(ov)
+    subdiv = ov.pop("_subdiv", 10)
+    settings = replace(scenes.settings_for(cfg), **ov)
+    return _scene(cfg.scene, subdiv), settings, cfg.camera(), frames, accumulate
+
+
 def packed_digest(packed) -> str:
     h = hashlib.sha256()
     for k, v in packed.as_numpy().items():

@@ -1,0 +1,106 @@
+"""The native host: the C++ HalogenRenderPass (include/halogen_render_pass.hpp) restating the reference's C# host
+surface (HalogenRenderPass.cs), driven by halogen-pathtracer_amd/host/halogen_render.
+
+CPU: its uniform derivation (clamp_settings + make_params, RP:169-231 / RP:359-401) produces the same hg_params
+bytes as the Python mirror (halogen/render_pass.py) over the parity cases and clamping edge cases.
+GPU: a render through the C++ pass is bit-identical to the golden images and counters of the CPU oracle."""
+import json
+import subprocess
+from dataclasses import replace
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import cases
+from halogen import host_files, render_pass as rp, scenes
+from halogen.unity import Transform
+
+ROOT = Path(__file__).resolve().parents[1]
+CLI = ROOT / "halogen-pathtracer_amd" / "host" / "halogen_render"
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+@pytest.fixture(scope="module")
+def cli(built):
+    if not CLI.exists():
+        subprocess.run(["make", "-s", "-C", str(ROOT / "halogen-pathtracer_amd"), str(CLI)], check=True)
+    return CLI
+
+
+def _python_params(settings, camera, frame_count, n_spheres, n_meshes):
+    s = rp.clamp_settings(settings)
+    return bytes(rp.make_params(s, camera, frame_count, n_spheres, n_meshes, s["UseEnvironmentCubemap"]))
+
+
+def _cpp_params(cli, tmp_path, settings, camera, frame_count, n_spheres, n_meshes):
+    cfg = tmp_path / "p.cfg"
+    host_files.write_config(settings, camera, cfg, frame_count=frame_count, n_spheres=n_spheres, n_meshes=n_meshes,
+                            cubemap_path="cube.hgcube" if settings.environmentCubemap is not None else None)
+    out = subprocess.run([str(cli), "params", str(cfg)], check=True, capture_output=True, text=True).stdout.strip()
+    return bytes.fromhex(out)
+
+
+def _variants():
+    base = scenes.settings_for(scenes.CONFIGS["C1"])
+    yield "defaults", rp.HalogenSettings(), scenes.cornell_camera(256, 256)
+    for name in cases.CASES:
+        _, settings, camera, _, _ = cases.setup_host(name)
+        yield name, settings, camera
+    edge = dict(SamplesPerPixel=0, MaxBounces=-3, DiffuseBounces=-1, GlossyBounces=-2, TransmissionBounces=-5,
+                FilterRadius=-1.0, NearPlaneDistance=0.0, FarPlaneDistance=-10.0, FocalPlaneDistance=-2.0,
+                ApertureAngle=120.0, EnvironmentMipLevel=7, MaxAccumulatedFrames=0, TriangleDebugDisplayRange=0,
+                BoxDebugDisplayRange=-4)
+    yield "clamped", replace(base, **edge), scenes.cornell_camera(320, 200)
+    yield "debug_first", replace(base, DebugMode="Normal", FirstInteractionOnly=True), scenes.cornell_camera(33, 17)
+    yield "no_accumulate", replace(base, Accumulate=False), scenes.glass_camera(1920, 1080)
+    rng = np.random.default_rng(3)
+    for k in range(6):
+        q = rng.normal(0, 1, 4)
+        cam = rp.Camera(Transform(position=rng.normal(0, 5, 3), rotation=q / np.linalg.norm(q)),
+                        fieldOfView=float(rng.uniform(10, 120)), pixelWidth=int(rng.integers(8, 4000)),
+                        pixelHeight=int(rng.integers(8, 3000)))
+        st = replace(base, ApertureAngle=float(rng.uniform(0, 10)), FocalPlaneDistance=float(rng.uniform(0.5, 20)),
+                     FilterRadius=float(rng.uniform(0, 3)), NearPlaneDistance=float(rng.uniform(0.01, 1)))
+        yield f"random{k}", st, cam
+
+
+@pytest.mark.parametrize("frame_count", [1, 7])
+def test_cpp_make_params_matches_python(cli, tmp_path, frame_count):
+    for name, settings, camera in _variants():
+        py = _python_params(settings, camera, frame_count, 3, 9)
+        cpp = _cpp_params(cli, tmp_path, settings, camera, frame_count, 3, 9)
+        assert cpp == py, name
+
+
+def test_cpp_host_rejects_bad_input(cli, tmp_path):
+    (tmp_path / "bad.cfg").write_text("NoSuchSetting 1\n")
+    r = subprocess.run([str(cli), "params", str(tmp_path / "bad.cfg")], capture_output=True, text=True)
+    assert r.returncode == 2 and "unknown key" in r.stderr
+    (tmp_path / "bad.hgscene").write_bytes(b"NOTSCENE")
+    r = subprocess.run([str(cli), "render", str(tmp_path / "bad.hgscene"), str(tmp_path / "bad.cfg"),
+                        str(tmp_path / "o.f32")], capture_output=True, text=True)
+    assert r.returncode == 2 and "HGSCENE1" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1_64", "c1_48_noacc", "c1_32_aperture", "glass_64x36", "dragon1_64x36"])
+def test_gpu_cpp_render_pass_matches_golden(gpu, cli, tmp_path, name):
+    meta = json.loads((GOLD / f"{name}.json").read_text())
+    packed, settings, camera, frames, _ = cases.setup_host(name)
+    host_files.write_scene(packed, tmp_path / "s.hgscene")
+    cube = None
+    if settings.useHDRISky and settings.environmentCubemap is not None:
+        cube = tmp_path / "c.hgcube"
+        host_files.write_cubemap(settings.environmentCubemap, cube)
+    host_files.write_config(settings, camera, tmp_path / "s.cfg", frames=frames,
+                            cubemap_path=str(cube) if cube else None)
+    r = subprocess.run([str(cli), "render", str(tmp_path / "s.hgscene"), str(tmp_path / "s.cfg"),
+                        str(tmp_path / "img.f32")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    cnt = json.loads(r.stdout)
+    img = np.fromfile(tmp_path / "img.f32", dtype=np.float32).reshape(camera.pixelHeight, camera.pixelWidth, 4)
+    ref = np.load(GOLD / f"{name}.npz")["image"]
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), name
+    for k in ("paths", "rays", "tri_tests", "aabb_tests"):
+        assert cnt[k] == meta["counters"][k], (k, cnt[k], meta["counters"][k])
