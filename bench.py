@@ -267,6 +267,11 @@ def main():
             "mrays_per_s": totals["rays"] / dt / 1e6 if counters_ok else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         # the PMC-measured DRAM-side bytes per launch over the same launch time (the working set
+                         # is cache-resident, so this is far below the algorithmic figure)
+                         "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and mean_launch_s > 0 else None,
+                         "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS
+                         if traffic and mean_launch_s > 0 else None,
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_launch_ms": mean_launch_s * 1e3,
                          "kernel": kernel_symbol},
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
