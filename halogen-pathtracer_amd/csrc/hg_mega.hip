@@ -366,6 +366,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         trav_begin(kp, ray, tv, c);
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
+#if HG_SHADE_PRIO >= 2
+    __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);  // traversal waits on memory: its waves issue first
+#endif
     while (__any(work)) {
         // ---- traversal rounds until few lanes are left traversing
         if (kCounters) cyc_trav -= wave_clock();
@@ -381,6 +384,11 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             cyc_trav += t;
             cyc_shade -= t;
         }
+#if HG_SHADE_PRIO == 1
+        __builtin_amdgcn_s_setprio(1);
+#elif HG_SHADE_PRIO >= 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
         // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
         // (rays that finish at once — everything culled — shade again in this loop while at least
         // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
@@ -486,6 +494,11 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             if (kCounters) tp = phase_mark(kp, 14, tp);
 #endif
         }
+#if HG_SHADE_PRIO == 1
+        __builtin_amdgcn_s_setprio(0);
+#elif HG_SHADE_PRIO >= 2
+        __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);
+#endif
         if (kCounters) cyc_shade += wave_clock();
     }
     if (kCounters) {
