@@ -96,6 +96,9 @@
 #ifndef HG_SHADE_PRIO
 #define HG_SHADE_PRIO 2  // streaming kernel wave priority (s_setprio): 1 = raised while shading, k >= 2 = raised to
 #endif                    // k-1 while traversing (C3 2,097 -> 2,111, k = 2/3/4 alike; tools/sweep67-68.txt)
+#ifndef HG_REGEN_PRIO
+#define HG_REGEN_PRIO 1  // regenerating kernel: wave priority raised during get_ray_intersection (C2 +1 %, C5 +2 %,
+#endif                   // tools/sweep69.txt)
 #ifndef HG_CAMERA_PASS
 #define HG_CAMERA_PASS 0  // streaming kernel, spp 1: primary rays precomputed by a coherent pass (hg_camera_rays)
 #endif

@@ -142,7 +142,13 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         const bool was_work = work;
         uint64_t t1 = 0;
         if (work) {
+#if HG_REGEN_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
             const Hit hit = intersect(kp, ray, c, stk);
+#if HG_REGEN_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             if (kCounters) t1 = wave_clock();
             c.shade_rounds += wave_once();
             bool alive = false;
