@@ -774,6 +774,10 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         int split = 1;
         if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
+            // the streaming kernel with >= 6 waves per resident slot already drains well unsplit: C3 1080p at N=1
+            // 2,111 (auto, split 3) -> 2,177 (split 1); a rank's share at N=2/4 (3.2 / 1.6 per slot) keeps the
+            // automatic rule, where split 2-6 lost 2-7 % (tools/sweep71.txt)
+            else if (stream_k && units >= 6 * resident) split = 1;
             else split = int(std::min<int64_t>(n_frames, (16 * resident + units - 1) / units));
         }
         int chunk_max = HG_REGEN_MAX_CHUNK;
