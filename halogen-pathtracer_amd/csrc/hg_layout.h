@@ -67,7 +67,7 @@
 #define HG_STREAM_RESHADE 16  // streaming kernel: repeat the shading pass while at least this many lanes need it
 #endif
 #ifndef HG_STREAM_DESCENT_T
-#define HG_STREAM_DESCENT_T 6  // the same for the streaming kernel (tools/sweep42.txt)
+#define HG_STREAM_DESCENT_T 8  // the same for the streaming kernel (tools/sweep42.txt; 8 with the unsplit launch, sweep74)
 #endif
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16

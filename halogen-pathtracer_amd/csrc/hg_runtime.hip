@@ -746,7 +746,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (deep_blas ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
                                                      : c->kernel;
     const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
-    // relaxed descent threshold: 3 for the regen / lockstep kernels, 4 for the streaming one (tools/sweep38.txt)
+    // relaxed descent threshold: 3 for the regen / lockstep kernels, HG_STREAM_DESCENT_T for the streaming one
     kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
                    : !deep_blas      ? 0u
                    : kern == HG_KERNEL_MEGA_STREAM ? uint32_t(HG_STREAM_DESCENT_T)
