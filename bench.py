@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
+    ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
@@ -150,6 +151,8 @@ def main():
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
     if args.frame_split >= 0:
         ctx.set_option(abi.HG_OPT_FRAME_SPLIT, args.frame_split)
+    if args.tile_order >= 0:
+        ctx.set_option(abi.HG_OPT_TILE_ORDER, args.tile_order)
     if args.descent_t >= -1:
         ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)

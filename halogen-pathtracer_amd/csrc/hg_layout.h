@@ -108,6 +108,9 @@
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
+#ifndef HG_TILE_ORDER
+#define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
+#endif
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
 #endif
@@ -154,6 +157,11 @@ struct HgKernelParams {
     float4* __restrict__ cam_a;
     float2* __restrict__ cam_b;
     float4* __restrict__ pool;  // path-pool kernel: per-wave path slots (hg_pool.hip)
+    // cost-ordered dispatch (regen / stream kernels): wave w traces local tile tile_order[w % n_local_tiles] (null:
+    // tile w % n_local_tiles) and adds its wave-clock cost to tile_cost[tile] (null: not recorded).  Any permutation
+    // gives the same image: tiles are independent and each tile's frames keep their order.
+    uint32_t* __restrict__ tile_cost;
+    const uint32_t* __restrict__ tile_order;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane

@@ -99,14 +99,85 @@ struct LaneVec {
 };
 constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
 
+// Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
+// written by hg_order_tiles before this launch and never during it).
+__device__ __forceinline__ int ordered_tile(const HgKernelParams& kp, uint32_t w) {
+    if (!kp.tile_order) return int(w);
+#if HG_TILE_ORDER_SCALAR
+    typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+    return int(((cu32p)(uintptr_t)kp.tile_order)[__builtin_amdgcn_readfirstlane(w)]);
+#else
+    return int(kp.tile_order[w]);
+#endif
+}
+// The wave's clock time, added to its tile's cost for the next launch's order (1/64 cycle units: a tile's sum stays
+// far below 2^32 for any launch the frame chunking allows).  The start time and the tile wait in LDS, not in
+// registers that would stay live across the whole kernel.
+__shared__ uint64_t hg_wave_t0[4];
+__shared__ uint32_t* hg_wave_cost[4];  // &tile_cost[tile], null: not recorded
+__device__ __forceinline__ void tile_cost_begin(const HgKernelParams& kp, uint32_t lane, int tile, bool valid) {
+    if (lane == 0) {
+        hg_wave_cost[threadIdx.x >> 6] = kp.tile_cost && valid ? kp.tile_cost + tile : nullptr;
+        hg_wave_t0[threadIdx.x >> 6] = wave_clock();
+    }
+}
+__device__ __forceinline__ void record_tile_cost(uint32_t lane) {
+    if (lane != 0) return;
+    uint32_t* const p = hg_wave_cost[threadIdx.x >> 6];
+    if (p) atomicAdd(p, uint32_t((wave_clock() - hg_wave_t0[threadIdx.x >> 6]) >> 6));
+}
+
+// One workgroup: tile_order = the local tiles by descending cost (1024 linear cost buckets, counting sort; the
+// order inside a bucket is arbitrary, which no image depends on), then the costs are cleared for the next launch.
+// A launch with no recorded cost keeps the identity order.
+__global__ __launch_bounds__(1024) void hg_order_tiles(uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+                                                       uint32_t n) {
+    __shared__ uint32_t bucket_start[1024];
+    __shared__ uint32_t cmax;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) cmax = 0;
+    bucket_start[t] = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t i = t; i < n; i += 1024) m = max(m, cost[i]);
+    atomicMax(&cmax, m);
+    __syncthreads();
+    const uint32_t top = cmax;
+    // bucket 0 = most expensive
+    auto bucket = [top](uint32_t c) { return 1023u - uint32_t((uint64_t(c) * 1024u) / (uint64_t(top) + 1u)); };
+    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&bucket_start[bucket(cost[i])], 1u);
+    __syncthreads();
+    if (t == 0) {  // exclusive prefix sum over the 1024 buckets
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < 1024u; ++b) {
+            const uint32_t k = bucket_start[b];
+            bucket_start[b] = run;
+            run += k;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += 1024) {
+        const uint32_t c = cost[i];
+        order[atomicAdd(&bucket_start[bucket(c)], 1u)] = i;
+        cost[i] = 0;
+    }
+}
+
+hipError_t hg_launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(hg_order_tiles, dim3(1), dim3(1024), 0, stream, cost, order, n);
+    return hipGetLastError();
+}
+
 template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
-    const int local_tile = int(gw % nlt);
+    const int local_tile = ordered_tile(kp, gw % nlt);
     const uint32_t chunk = gw / nlt;
+    tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
@@ -234,6 +305,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
             cyc_shade += t2 - t1u;
         }
     }
+    record_tile_cost(lane);
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * uint32_t(kp.n_meshes),
                                c.rays * uint32_t(kp.n_spheres), c.hits, c.node_rounds, c.tri_rounds};
@@ -334,8 +406,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
-    const int local_tile = int(gw % nlt);
+    const int local_tile = ordered_tile(kp, gw % nlt);
     const uint32_t chunk = gw / nlt;
+    tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
     const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
@@ -507,6 +580,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 #endif
         if (kCounters) cyc_shade += wave_clock();
     }
+    record_tile_cost(lane);
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
                                c.node_rounds, c.tri_rounds};

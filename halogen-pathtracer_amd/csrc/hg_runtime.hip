@@ -23,6 +23,7 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
+hipError_t hg_launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream);
 hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream);
 hipError_t hg_launch_mega_pool(const HgKernelParams& kp, bool counters, hipStream_t stream);
 uint32_t hg_pool_slots();
@@ -79,6 +80,8 @@ struct hg_ctx {
     DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     DevBuf pool;                 // path-pool kernel: per-wave path slots
     DevBuf cam_a, cam_b;         // camera-ray pass: primary rays of this launch chunk
+    DevBuf tile_cost, tile_order;  // cost-ordered dispatch: per local tile, wave-clock cost / dispatch order
+    bool tile_cost_valid = false;  // tile_cost holds the previous regen/stream launch's costs for this tiling
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -93,6 +96,7 @@ struct hg_ctx {
     int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0, refill = 32;
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
     int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
+    int32_t tile_order_on = HG_TILE_ORDER;  // HG_OPT_TILE_ORDER
 };
 
 namespace {
@@ -263,6 +267,7 @@ int alloc_target(hg_ctx* c) {
     c->tiles_y = (c->H + HG_TILE - 1) / HG_TILE;
     const int64_t total = int64_t(c->tiles_x) * c->tiles_y;
     c->n_local_tiles = total > c->rank ? int32_t((total - c->rank + c->n_ranks - 1) / c->n_ranks) : 0;
+    c->tile_cost_valid = false;
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     const size_t slots = size_t(c->n_local_tiles) * 64;
     for (DevBuf* b : {&c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col, &c->wf_sum, &c->wf_tuvo})
@@ -397,7 +402,8 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool, &c->cam_a, &c->cam_b})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool, &c->cam_a, &c->cam_b,
+                      &c->tile_cost, &c->tile_order})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -829,11 +835,37 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             kc.frame_color = static_cast<float4*>(c->frame_color.p);
             kc.cam_a = cam_pass ? static_cast<float4*>(c->cam_a.p) : nullptr;
             kc.cam_b = cam_pass ? static_cast<float2*>(c->cam_b.p) : nullptr;
+            // cost-ordered dispatch: the previous launch's per-tile wave times order this launch's tiles, most
+            // expensive first, so the launch's drain tail holds the cheap tiles (any order gives the same image)
+            kc.tile_cost = nullptr;
+            kc.tile_order = nullptr;
+            if (c->tile_order_on && tiles > 0 && !pool_k) {
+                const size_t tb = size_t(tiles) * sizeof(uint32_t);
+                if (int rc = ensure(c, c->tile_cost, tb)) {
+                    c->free_events.push_back(ev);
+                    return rc;
+                }
+                if (int rc = ensure(c, c->tile_order, tb)) {
+                    c->free_events.push_back(ev);
+                    return rc;
+                }
+                kc.tile_cost = static_cast<uint32_t*>(c->tile_cost.p);
+            }
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
-                if (cam_pass) e = hg_launch_camera_rays(kc, c->stream);
+                if (kc.tile_cost) {
+                    if (c->tile_cost_valid) {  // order from the recorded costs, which it then clears
+                        e = hg_launch_order_tiles(kc.tile_cost, static_cast<uint32_t*>(c->tile_order.p),
+                                                  uint32_t(tiles), c->stream);
+                        kc.tile_order = static_cast<const uint32_t*>(c->tile_order.p);
+                    } else {
+                        e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(uint32_t), c->stream);
+                    }
+                    c->tile_cost_valid = e == hipSuccess;
+                }
+                if (e == hipSuccess && cam_pass) e = hg_launch_camera_rays(kc, c->stream);
                 if (e == hipSuccess)
                     e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
                     : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
@@ -982,6 +1014,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_DESCENT_T:
             if (value < -1 || value > 64) return fail(c, HG_E_INVALID, "descent threshold must be -1 (auto)..64");
             c->descent_t = value;
+            return HG_OK;
+        case HG_OPT_TILE_ORDER:
+            c->tile_order_on = value ? 1 : 0;
+            c->tile_cost_valid = false;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

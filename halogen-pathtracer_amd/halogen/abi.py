@@ -93,6 +93,7 @@ HG_KERNEL_MEGA, HG_KERNEL_WAVEFRONT, HG_KERNEL_MEGA_REGEN, HG_KERNEL_MEGA_STREAM
 HG_KERNEL_AUTO = 5
 HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING, HG_OPT_REFILL, HG_OPT_FRAME_SPLIT = 1, 2, 3, 4, 5, 6
 HG_OPT_DESCENT_T = 7
+HG_OPT_TILE_ORDER = 8
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [

@@ -191,9 +191,11 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile.
  * HG_OPT_DESCENT_T: traversal descent loop, leave it once at most this many lanes are still descending (the others
  *   test their leaves meanwhile; each lane's own step order is unchanged): -1 = automatic (for BLAS deeper than 16
- *   levels 3, or 4 with the streaming kernel; else 0 = classic while-while), 0..64 = fixed. */
+ *   levels 3, or 8 with the streaming kernel; else 0 = classic while-while), 0..64 = fixed.
+ * HG_OPT_TILE_ORDER: regenerating / streaming kernels, 1 (default) = each launch dispatches its tiles by descending
+ *   wave time in the previous launch (shorter drain tail; same image), 0 = tile-index order. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7 };
+       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8 };
 
 int hg_abi_version(void);
 

@@ -228,3 +228,30 @@ def test_gpu_auto_kernel_choice(gpu):
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), False)
     _, cnt = gpu_render(packed, params, 2, True, None, kernel="auto")
     assert cnt["last_kernel"] == abi.HG_KERNEL_MEGA_STREAM
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["regen", "stream"])
+@pytest.mark.parametrize("name", ["c1_64", "glass_64x36", "dragon1_64x36"])
+def test_gpu_tile_order_bit_exact(gpu, name, kernel):
+    """Cost-ordered dispatch (HG_OPT_TILE_ORDER): every launch after the first traces its tiles in the order of the
+    previous launch's wave times.  Several render calls (so later launches use a recorded order), unsplit and split,
+    whole image and one rank's share, give the image and counters of the tile-index order."""
+    packed, params, cube, frames, acc = cases.setup(name)
+    for tiling in (None, (1, 3)):
+        for split in (1, 3):
+            out = []
+            for on in (0, 1):
+                with abi.Context(0) as ctx:
+                    ctx.set_option(abi.HG_OPT_TILE_ORDER, on)
+                    ctx.set_option(abi.HG_OPT_FRAME_SPLIT, split)
+                    out.append(gpu_render(packed, params, 8, acc, cube, tiling=tiling, ctx=ctx, splits=[1, 2, 3, 2],
+                                          kernel=kernel))
+            assert_bitwise(out[1][0], out[0][0], f"{name} {kernel} tiling {tiling} split {split}")
+            for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+                assert out[1][1][k] == out[0][1][k], (k, out[1][1][k], out[0][1][k])
+    if name == "c1_64":
+        ref, _ = hg_oracle.render(packed, params, 8, acc)
+        with abi.Context(0) as ctx:
+            img, _ = gpu_render(packed, params, 8, acc, cube, ctx=ctx, splits=[2, 2, 4], kernel=kernel)
+        assert_bitwise(img, ref, f"{kernel} ordered vs oracle")

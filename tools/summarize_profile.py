@@ -51,6 +51,18 @@ def main():
         stats[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                    "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
 
+    # per-launch durations from the kernel trace: the bench's first launch (warmup) runs in tile-index order, the
+    # later ones in the cost order it recorded (HG_OPT_TILE_ORDER), so the timed launches are the ones after it
+    trace_csv = src / f"{a.tag}_stats" / "stats_kernel_trace.csv"
+    if trace_csv.exists():
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(trace_csv)):
+            durs[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        for k, v in durs.items():
+            if k in stats:
+                stats[k]["launch_ms"] = v
+                if len(v) > 1:
+                    stats[k]["avg_ms_after_first"] = sum(v[1:]) / (len(v) - 1)
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     calls = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in sorted(glob.glob(str(src / f"{a.tag}_*" / "*_counter_collection.csv"))):
