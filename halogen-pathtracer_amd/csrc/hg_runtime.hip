@@ -767,7 +767,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
         const int mblock = pool_k ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
-        // about 16x as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
+        // about 12x (formerly 16x) as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
         // (bit-identical).  Measured (tools/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
         // rank's share at N=8 314 -> 1212.
@@ -784,7 +784,9 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             // 2,111 (auto, split 3) -> 2,177 (split 1); a rank's share at N=2/4 (3.2 / 1.6 per slot) keeps the
             // automatic rule, where split 2-6 lost 2-7 % (tools/sweep71.txt)
             else if (stream_k && units >= 6 * resident) split = 1;
-            else split = int(std::min<int64_t>(n_frames, (16 * resident + units - 1) / units));
+            // about 12 launches' worth of wave slots (16 before the cost-ordered dispatch; with it, a rank's share
+            // at N=2/4 gains 2.6 / 1.2 %, C2 / C5 0.8 / 1.2 %, N=8 is flat over 16-26: tools/sweep77-78.txt)
+            else split = int(std::min<int64_t>(n_frames, (12 * resident + units - 1) / units));
         }
         int chunk_max = HG_REGEN_MAX_CHUNK;
         if (split > 1) {
