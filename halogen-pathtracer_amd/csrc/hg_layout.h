@@ -111,6 +111,9 @@
 #ifndef HG_TILE_ORDER
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif
+#ifndef HG_UNIT_TILE_MAJOR
+#define HG_UNIT_TILE_MAJOR 1  // cost order: a tile's frame chunks on consecutive waves (hg_mega.hip wave_unit; tools/sweep81.txt)
+#endif
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
 #endif

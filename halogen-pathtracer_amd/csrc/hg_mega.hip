@@ -110,6 +110,24 @@ __device__ __forceinline__ int ordered_tile(const HgKernelParams& kp, uint32_t w
     return int(kp.tile_order[w]);
 #endif
 }
+// The wave's work unit (tile, frame chunk).  Tile-index order: chunk-major (wave w: tile w mod tiles, chunk
+// w / tiles).  Cost order with HG_UNIT_TILE_MAJOR: tile-major (wave w: tile order[w / split], chunk w mod split), so
+// a tile's chunks run side by side and the most expensive tiles' chunks all start first.  Waves past the last unit
+// get chunk = split (no work).
+__device__ __forceinline__ void wave_unit(const HgKernelParams& kp, uint32_t gw, uint32_t nlt, uint32_t split,
+                                          int& tile, uint32_t& chunk) {
+#if HG_UNIT_TILE_MAJOR
+    if (kp.tile_order) {
+        const uint32_t w = gw / split;
+        tile = w < nlt ? ordered_tile(kp, w) : 0;
+        chunk = w < nlt ? gw % split : split;
+        return;
+    }
+#endif
+    tile = ordered_tile(kp, gw % nlt);
+    chunk = gw / nlt;
+}
+
 // The wave's clock time, added to its tile's cost for the next launch's order (1/64 cycle units: a tile's sum stays
 // far below 2^32 for any launch the frame chunking allows).  The start time and the tile wait in LDS, not in
 // registers that would stay live across the whole kernel.
@@ -175,8 +193,9 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
-    const int local_tile = ordered_tile(kp, gw % nlt);
-    const uint32_t chunk = gw / nlt;
+    int local_tile;
+    uint32_t chunk;
+    wave_unit(kp, gw, nlt, split, local_tile, chunk);
     tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
@@ -406,8 +425,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
-    const int local_tile = ordered_tile(kp, gw % nlt);
-    const uint32_t chunk = gw / nlt;
+    int local_tile;
+    uint32_t chunk;
+    wave_unit(kp, gw, nlt, split, local_tile, chunk);
     tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);

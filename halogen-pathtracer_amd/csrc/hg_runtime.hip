@@ -767,7 +767,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
         const int mblock = pool_k ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
-        // about 12x (formerly 16x) as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
+        // about 6x (formerly 16x, 12x) as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
         // (bit-identical).  Measured (tools/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
         // rank's share at N=8 314 -> 1212.
@@ -780,13 +780,11 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         int split = 1;
         if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
-            // the streaming kernel with >= 6 waves per resident slot already drains well unsplit: C3 1080p at N=1
-            // 2,111 (auto, split 3) -> 2,177 (split 1); a rank's share at N=2/4 (3.2 / 1.6 per slot) keeps the
-            // automatic rule, where split 2-6 lost 2-7 % (tools/sweep71.txt)
-            else if (stream_k && units >= 6 * resident) split = 1;
-            // about 12 launches' worth of wave slots (16 before the cost-ordered dispatch; with it, a rank's share
-            // at N=2/4 gains 2.6 / 1.2 %, C2 / C5 0.8 / 1.2 %, N=8 is flat over 16-26: tools/sweep77-78.txt)
-            else split = int(std::min<int64_t>(n_frames, (12 * resident + units - 1) / units));
+            // about 6 launches' worth of wave slots: with the cost order and a tile's chunks on consecutive waves
+            // (wave_unit), fewer, longer waves win: a rank's share at N=2 split 2 vs 4 -> 2,409 vs 2,308, N=8 8 vs 16
+            // -> 2,440 vs 2,337, C2 / C5 2 vs 3 -> +1.5 / +2.7 %, C3 at N=1 stays unsplit (tools/sweep82-83.txt;
+            // the multiplier was 16, then 12 with the chunk-major cost order)
+            else split = int(std::min<int64_t>(n_frames, (6 * resident + units - 1) / units));
         }
         int chunk_max = HG_REGEN_MAX_CHUNK;
         if (split > 1) {

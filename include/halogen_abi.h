@@ -187,7 +187,7 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).
  * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then
- *   blended in frame order, bit-identical): 0 = automatic (about 12 launches' worth of the GPU's wave slots per
+ *   blended in frame order, bit-identical): 0 = automatic (about 6 launches' worth of the GPU's wave slots per
  *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile.
  * HG_OPT_DESCENT_T: traversal descent loop, leave it once at most this many lanes are still descending (the others
  *   test their leaves meanwhile; each lane's own step order is unchanged): -1 = automatic (for BLAS deeper than 16
