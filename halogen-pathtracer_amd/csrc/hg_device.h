@@ -474,7 +474,12 @@ __device__ __forceinline__ float bperm_f(int addr, float x) {
 // other triangles, and `closest` only falls, so the loop ends on the first triangle (in leaf order) of minimal t
 // among those with t < best_t at the leaf's start.  t > 1e-4 is positive, so its bit pattern orders like its
 // value, and the lower triangle index wins a tie: the key minimum is that triangle.  Counters are the same
-// (one triangle test per pair).  Every lane of the wave must be active.
+// (one triangle test per pair).
+// Precondition: every lane of the wave is active (the DPP scans and ds_bpermute read other lanes' registers; under a
+// partial EXEC a disabled lane's register is stale and the prefix sums skip it).  The streaming kernel meets it by
+// construction: trav_step runs at the top level of loops whose exits are wave-uniform (ballot counts).  Debug builds
+// (HG_CHECK_EXEC=1) check it and take the sequential leaf loop when a lane is off (returns false); the check is
+// compiled out of the product build because keeping the fallback loop live costs the kernel 16 B/lane of scratch.
 struct LeafRay {  // the lane's side of a leaf test: its mesh-local ray and running best hit
     const f3& lo;
     const f3& ld;
@@ -485,12 +490,15 @@ struct LeafRay {  // the lane's side of a leaf test: its mesh-local ray and runn
     uint32_t& best_mesh;
     uint32_t mi;
 };
-__device__ __forceinline__ void leaf_dist(const HgKernelParams& kp, const LeafRay& t, Counters& c, const LeafShare& ls,
+__device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRay& t, Counters& c, const LeafShare& ls,
                                           uint32_t first, uint32_t n) {
+#if HG_CHECK_EXEC
+    if (__ballot(1) != ~0ull) return false;  // partial EXEC: the sequential loop instead (see above)
+#endif
     const uint32_t lane = __lane_id();
     const uint32_t incl = wave_incl_add(n);
     const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
-    if (total == 0u) return;
+    if (total == 0u) return true;
     const uint32_t start = incl - n;
     const uint32_t fo = first - start;  // owner's triangle index = fo + pair index (mod 2^32)
     if (n) *ls.key(lane) = ~0ull;
@@ -534,6 +542,7 @@ __device__ __forceinline__ void leaf_dist(const HgKernelParams& kp, const LeafRa
             t.best_mesh = t.mi;
         }
     }
+    return true;
 }
 
 // get_ray_scene_intersection_mesh, :378-472.
@@ -873,10 +882,11 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         }
         // distribute only when the longest leaf would take enough sequential rounds to pay for the exchange
         if (HG_LEAF_DIST_MIN <= 1 || uint32_t(__builtin_amdgcn_readlane(int(wave_incl_max(n)), 63)) >= HG_LEAF_DIST_MIN) {
-            leaf_dist(kp, LeafRay{t.lo, t.ld, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, t.mi}, c, ls,
-                      first, n);
-            if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
-            seq_leaf = false;
+            if (leaf_dist(kp, LeafRay{t.lo, t.ld, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, t.mi}, c,
+                          ls, first, n)) {
+                if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+                seq_leaf = false;
+            }
         }
     }
 #else

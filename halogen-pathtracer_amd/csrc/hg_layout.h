@@ -52,7 +52,7 @@
 #define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~120 VGPRs)
 #endif
 #ifndef HG_STREAM_TMIN
-#define HG_STREAM_TMIN 12  // streaming kernel: shade once at most this many lanes are still traversing (tools/sweep54.txt)
+#define HG_STREAM_TMIN 12  // streaming kernel: shade once at most this many lanes are still traversing (tools/sweeps/sweep54.txt)
 #endif
 #ifndef HG_RCP_NORMALIZE
 #define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)
@@ -67,7 +67,7 @@
 #define HG_STREAM_RESHADE 16  // streaming kernel: repeat the shading pass while at least this many lanes need it
 #endif
 #ifndef HG_STREAM_DESCENT_T
-#define HG_STREAM_DESCENT_T 8  // the same for the streaming kernel (tools/sweep42.txt; 8 with the unsplit launch, sweep74)
+#define HG_STREAM_DESCENT_T 8  // the same for the streaming kernel (tools/sweeps/sweep42.txt; 8 with the unsplit launch, sweep74)
 #endif
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16
@@ -83,22 +83,22 @@
 #endif
 #ifndef HG_TRI_PREFETCH
 #define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
-#endif                     // (regen: C2 -13 %, C5 -16 %: the registers spill; tools/sweep47.txt)
+#endif                     // (regen: C2 -13 %, C5 -16 %: the registers spill; tools/sweeps/sweep47.txt)
 #ifndef HG_STREAM_TRI_PREFETCH
 #define HG_STREAM_TRI_PREFETCH 1  // the same in the streaming kernel's leaf loop: C3 +3 % at no register cost
 #endif
 #ifndef HG_LEAF_DIST
 #define HG_LEAF_DIST 1  // streaming traversal: a round's (ray, triangle) pairs dealt over all 64 lanes, LDS min-reduce
-#endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweep52.txt)
+#endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweeps/sweep52.txt)
 #ifndef HG_LEAF_DIST_MIN
 #define HG_LEAF_DIST_MIN 1  // ... only when the wave's longest leaf has at least this many triangles (1: always;
 #endif                      // 2 / 3 measured 2066 / 2063)
 #ifndef HG_SHADE_PRIO
 #define HG_SHADE_PRIO 2  // streaming kernel wave priority (s_setprio): 1 = raised while shading, k >= 2 = raised to
-#endif                    // k-1 while traversing (C3 2,097 -> 2,111, k = 2/3/4 alike; tools/sweep67-68.txt)
+#endif                    // k-1 while traversing (C3 2,097 -> 2,111, k = 2/3/4 alike; tools/sweeps/sweep67-68.txt)
 #ifndef HG_REGEN_PRIO
 #define HG_REGEN_PRIO 1  // regenerating kernel: wave priority raised during get_ray_intersection (C2 +1 %, C5 +2 %,
-#endif                   // tools/sweep69.txt)
+#endif                   // tools/sweeps/sweep69.txt)
 #ifndef HG_CAMERA_PASS
 #define HG_CAMERA_PASS 0  // streaming kernel, spp 1: primary rays precomputed by a coherent pass (hg_camera_rays)
 #endif
@@ -112,10 +112,13 @@
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif
 #ifndef HG_UNIT_TILE_MAJOR
-#define HG_UNIT_TILE_MAJOR 1  // cost order: a tile's frame chunks on consecutive waves (hg_mega.hip wave_unit; tools/sweep81.txt)
+#define HG_UNIT_TILE_MAJOR 1  // cost order: a tile's frame chunks on consecutive waves (hg_mega.hip wave_unit; tools/sweeps/sweep81.txt)
 #endif
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
+#endif
+#ifndef HG_CHECK_EXEC
+#define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif
 #ifndef HG_MEGA_LDS_STACK
 #define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
@@ -163,7 +166,7 @@ struct HgKernelParams {
     // cost-ordered dispatch (regen / stream kernels): wave w traces local tile tile_order[w % n_local_tiles] (null:
     // tile w % n_local_tiles) and adds its wave-clock cost to tile_cost[tile] (null: not recorded).  Any permutation
     // gives the same image: tiles are independent and each tile's frames keep their order.
-    uint32_t* __restrict__ tile_cost;
+    unsigned long long* __restrict__ tile_cost;  // s_memtime cycles per tile
     const uint32_t* __restrict__ tile_order;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;

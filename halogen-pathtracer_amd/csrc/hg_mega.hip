@@ -1,11 +1,10 @@
-// hg_mega.hip — the one-thread-per-pixel megakernel (variant HG_KERNEL_MEGA).
+// hg_mega.hip — the megakernels of the hot path: the streaming kernel (default for deep BLAS), the regenerating
+// kernel (default otherwise) and the lockstep kernel (HG_KERNEL_MEGA: debug views, large-maxBounces fallback).
 //
 // Reference: Assets/Scripts/Halogen Shaders/HalgoenCompute.compute, kernel HalogenCompute (:1015-1063) with
 // the accumulation blit (AccumulationShader.shader:27-34) fused as its epilogue.  One wave64 = one 8x8 pixel
-// tile, each lane runs all n_frames frames of its pixel back to back, the BLAS stack lives in LDS
-// ([depth][lane]).  It is the simplest faithful form of the hot path; the runtime uses it for the debug
-// views (modes 1-5 need per-path TriangleTests/AABBTests) and as the A/B baseline of the wavefront pipeline
-// (hg_wavefront.hip), which is the default for rendering.
+// tile; the BLAS stack lives in LDS ([depth][lane]).  The lockstep kernel below is the simplest faithful form:
+// each lane runs all n_frames frames of its pixel back to back.
 #include <hip/hip_runtime.h>
 
 #include "hg_device.h"
@@ -128,11 +127,11 @@ __device__ __forceinline__ void wave_unit(const HgKernelParams& kp, uint32_t gw,
     chunk = gw / nlt;
 }
 
-// The wave's clock time, added to its tile's cost for the next launch's order (1/64 cycle units: a tile's sum stays
-// far below 2^32 for any launch the frame chunking allows).  The start time and the tile wait in LDS, not in
-// registers that would stay live across the whole kernel.
+// The wave's clock time (s_memtime cycles), added to its tile's 64-bit cost for the next launch's order (no wrap for
+// any launch: 2^64 cycles).  The start time and the tile wait in LDS, not in registers that would stay live across
+// the whole kernel.
 __shared__ uint64_t hg_wave_t0[4];
-__shared__ uint32_t* hg_wave_cost[4];  // &tile_cost[tile], null: not recorded
+__shared__ unsigned long long* hg_wave_cost[4];  // &tile_cost[tile], null: not recorded
 __device__ __forceinline__ void tile_cost_begin(const HgKernelParams& kp, uint32_t lane, int tile, bool valid) {
     if (lane == 0) {
         hg_wave_cost[threadIdx.x >> 6] = kp.tile_cost && valid ? kp.tile_cost + tile : nullptr;
@@ -141,47 +140,81 @@ __device__ __forceinline__ void tile_cost_begin(const HgKernelParams& kp, uint32
 }
 __device__ __forceinline__ void record_tile_cost(uint32_t lane) {
     if (lane != 0) return;
-    uint32_t* const p = hg_wave_cost[threadIdx.x >> 6];
-    if (p) atomicAdd(p, uint32_t((wave_clock() - hg_wave_t0[threadIdx.x >> 6]) >> 6));
+    unsigned long long* const p = hg_wave_cost[threadIdx.x >> 6];
+    if (p) atomicAdd(p, (unsigned long long)(wave_clock() - hg_wave_t0[threadIdx.x >> 6]));
 }
 
-// One workgroup: tile_order = the local tiles by descending cost (1024 linear cost buckets, counting sort; the
-// order inside a bucket is arbitrary, which no image depends on), then the costs are cleared for the next launch.
-// A launch with no recorded cost keeps the identity order.
-__global__ __launch_bounds__(1024) void hg_order_tiles(uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
-                                                       uint32_t n) {
-    __shared__ uint32_t bucket_start[1024];
-    __shared__ uint32_t cmax;
-    const uint32_t t = threadIdx.x;
+// One workgroup of 1024 threads: tile_order = the local tiles by descending cost, STABLE (equal buckets keep
+// tile-index order, so the dispatch order of a launch is a deterministic function of the recorded costs), then the
+// costs are cleared for the next launch.  Counting sort over 1024 linear cost buckets (bucket 0 = most expensive):
+//   1. per-bucket counts over all tiles, exclusive prefix = each bucket's start;
+//   2. tiles in chunks of 1024 in index order: a tile's place = its bucket's running start + the number of earlier
+//      tiles of the same bucket in the chunk (inside a wave: a 10-ballot bucket match; across the chunk's 16 waves:
+//      per-wave bucket counts in LDS), then the running starts advance by the chunk's counts.
+// Costs all 0 (nothing recorded): every tile falls in one bucket and the order is the identity.
+__global__ __launch_bounds__(1024) void hg_order_tiles(unsigned long long* __restrict__ cost,
+                                                       uint32_t* __restrict__ order, uint32_t n) {
+    __shared__ uint32_t start[1024];        // running start of each bucket
+    __shared__ uint16_t wcount[16][1024];   // chunk: tiles of bucket b in wave w (then: exclusive prefix over w)
+    __shared__ unsigned long long cmax;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     if (t == 0) cmax = 0;
-    bucket_start[t] = 0;
+    start[t] = 0;
     __syncthreads();
-    uint32_t m = 0;
+    unsigned long long m = 0;
     for (uint32_t i = t; i < n; i += 1024) m = max(m, cost[i]);
     atomicMax(&cmax, m);
     __syncthreads();
-    const uint32_t top = cmax;
-    // bucket 0 = most expensive
-    auto bucket = [top](uint32_t c) { return 1023u - uint32_t((uint64_t(c) * 1024u) / (uint64_t(top) + 1u)); };
-    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&bucket_start[bucket(cost[i])], 1u);
+    const unsigned long long top = cmax;
+    // bucket = 1023 - floor(c * 1024 / (top + 1)), in 128-bit-safe form (c <= top)
+    auto bucket = [top](unsigned long long c) -> uint32_t {
+        const unsigned long long q = top / 1024u + 1u;  // c / q < 1024 for every c <= top
+        return 1023u - uint32_t(c / q);
+    };
+    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&start[bucket(cost[i])], 1u);
     __syncthreads();
-    if (t == 0) {  // exclusive prefix sum over the 1024 buckets
+    if (t == 0) {  // exclusive prefix sum over the buckets
         uint32_t run = 0;
         for (uint32_t b = 0; b < 1024u; ++b) {
-            const uint32_t k = bucket_start[b];
-            bucket_start[b] = run;
+            const uint32_t k = start[b];
+            start[b] = run;
             run += k;
         }
     }
     __syncthreads();
-    for (uint32_t i = t; i < n; i += 1024) {
-        const uint32_t c = cost[i];
-        order[atomicAdd(&bucket_start[bucket(c)], 1u)] = i;
-        cost[i] = 0;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (uint32_t base = 0; base < n; base += 1024u) {
+        const uint32_t i = base + t;
+        const bool valid = i < n;
+        const uint32_t b = valid ? bucket(cost[i]) : 1024u;  // 1024 (bit 10): past the end, no bucket
+        uint64_t same = ~0ull;
+        for (int bit = 0; bit < 11; ++bit) {  // lanes of this wave with the same bucket
+            const uint64_t set = __ballot((b >> bit) & 1u);
+            same &= ((b >> bit) & 1u) ? set : ~set;
+        }
+        const uint32_t rank = uint32_t(__popcll(same & lt_mask));
+        for (uint32_t w = 0; w < 16u; ++w) wcount[w][t] = 0;
+        __syncthreads();
+        if (valid && rank == 0) wcount[wave][b] = uint16_t(__popcll(same));
+        __syncthreads();
+        uint32_t run = 0;  // thread t = bucket t: exclusive prefix of its counts over the chunk's waves
+        for (uint32_t w = 0; w < 16u; ++w) {
+            const uint32_t k = wcount[w][t];
+            wcount[w][t] = uint16_t(run);
+            run += k;
+        }
+        __syncthreads();
+        if (valid) {
+            order[start[b] + wcount[wave][b] + rank] = i;
+            cost[i] = 0;
+        }
+        __syncthreads();
+        start[t] += run;
+        __syncthreads();
     }
 }
 
-hipError_t hg_launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
+hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(hg_order_tiles, dim3(1), dim3(1024), 0, stream, cost, order, n);
     return hipGetLastError();
@@ -373,13 +406,13 @@ hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) 
 
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     const int tiles_per_block = block / 64;
-    const int grid = (kp.n_local_tiles * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
+    const int64_t grid = (int64_t(kp.n_local_tiles) * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
     if (counters)
-        hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else
-        hipLaunchKernelGGL(hg_trace_regen_kernel<false>, dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL(hg_trace_regen_kernel<false>, dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     return hipGetLastError();
 }
 
@@ -620,19 +653,19 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     const int tiles_per_block = block / 64;
-    const int grid = (kp.n_local_tiles * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
+    const int64_t grid = (int64_t(kp.n_local_tiles) * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4 +
                        (HG_LEAF_DIST ? size_t(kLeafShareWords) * size_t(block) * 4 : 0);
     const bool cam = kp.cam_a != nullptr;
     if (counters && cam)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else if (counters)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else if (cam)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else
-        hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     return hipGetLastError();
 }
 
@@ -644,12 +677,12 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
     const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block);
     const bool dbg = kp.debug_mode != 0;
     if (counters && dbg)
-        hipLaunchKernelGGL((hg_trace_kernel<true, true>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_kernel<true, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else if (counters)
-        hipLaunchKernelGGL((hg_trace_kernel<true, false>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_kernel<true, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else if (dbg)
-        hipLaunchKernelGGL((hg_trace_kernel<false, true>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_kernel<false, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else
-        hipLaunchKernelGGL((hg_trace_kernel<false, false>), dim3(grid), dim3(block), lds, stream, kp);
+        hipLaunchKernelGGL((hg_trace_kernel<false, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     return hipGetLastError();
 }

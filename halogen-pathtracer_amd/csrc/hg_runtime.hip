@@ -23,8 +23,12 @@ hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hi
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
-hipError_t hg_launch_order_tiles(uint32_t* cost, uint32_t* order, uint32_t n, hipStream_t stream);
+hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, hipStream_t stream);
 hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream);
+#ifndef HG_WITH_VARIANTS
+#define HG_WITH_VARIANTS 0  // A/B variants (wavefront pipeline, path pool): make VARIANTS=1
+#endif
+#if HG_WITH_VARIANTS
 hipError_t hg_launch_mega_pool(const HgKernelParams& kp, bool counters, hipStream_t stream);
 uint32_t hg_pool_slots();
 uint32_t hg_pool_tiles();
@@ -35,7 +39,12 @@ hipError_t hg_wf_launch_shade(const HgKernelParams& kp, int grid, const uint32_t
                               uint32_t* q_out, uint32_t* n_out, hipStream_t s);
 int hg_wf_trace_blocks_per_cu(int block, size_t lds_bytes);
 size_t hg_wf_trace_lds_bytes(uint32_t stack_depth, int block);
-int64_t hg_wf_selftest_rcp(int64_t* tested);
+#else  // never reached: hg_set_option refuses the variants in this build
+static hipError_t hg_launch_mega_pool(const HgKernelParams&, bool, hipStream_t) { return hipErrorNotSupported; }
+static uint32_t hg_pool_slots() { return 1; }
+static uint32_t hg_pool_tiles() { return 1; }
+#endif
+int64_t hg_selftest_rcp_all(int64_t* tested);
 
 namespace {
 
@@ -270,6 +279,7 @@ int alloc_target(hg_ctx* c) {
     c->tile_cost_valid = false;
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     const size_t slots = size_t(c->n_local_tiles) * 64;
+#if HG_WITH_VARIANTS  // wavefront pipeline path state (152 B per pixel slot)
     for (DevBuf* b : {&c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col, &c->wf_sum, &c->wf_tuvo})
         if (int rc = ensure(c, *b, slots * sizeof(float4))) return rc;
     for (DevBuf* b : {&c->wf_st, &c->wf_st2})
@@ -278,6 +288,9 @@ int alloc_target(hg_ctx* c) {
         if (int rc = ensure(c, *b, slots * sizeof(uint2))) return rc;
     for (DevBuf* b : {&c->wf_q0, &c->wf_q1})
         if (int rc = ensure(c, *b, slots * sizeof(uint32_t))) return rc;
+#else
+    (void)slots;
+#endif
     release(c->acc);
     if (bytes) {
         hipError_t e = hipMalloc(&c->acc.p, bytes);
@@ -289,6 +302,7 @@ int alloc_target(hg_ctx* c) {
 }
 
 
+#if HG_WITH_VARIANTS
 // The bounce loop of the wavefront pipeline: gen, then (trace, shade) per iteration until the queue is empty.
 // The host does not wait for queue lengths: it launches ahead and polls pinned copies of the lengths a few
 // iterations behind, stopping once one of them reads zero (an empty queue stays empty).
@@ -360,6 +374,11 @@ int render_wavefront(hg_ctx* c, const HgKernelParams& kp) {
     }
     return HG_OK;
 }
+#else
+int render_wavefront(hg_ctx* c, const HgKernelParams&) {
+    return fail(c, HG_E_UNSUPPORTED, "wavefront pipeline not built (make VARIANTS=1)");
+}
+#endif
 
 }  // namespace
 
@@ -711,7 +730,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.n_local_tiles = c->n_local_tiles;
     kp.stack_depth = c->stack_depth;
     // deep BLAS (the dragon: 32 levels) descend in long, uneven runs: let the last few lanes pause while the rest
-    // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweep28-29.txt)
+    // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweeps/sweep28-29.txt)
 
     kp.refill_min = uint32_t(c->refill);
     kp.cube_size = c->cube_size;
@@ -747,7 +766,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (int rc = event_pair(c, ev)) return rc;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
     // HG_KERNEL_AUTO: the streaming kernel for deep BLAS (its resumable traversal pays off when a few lanes carry
-    // long traversals: C3 +6 %), the regenerating kernel otherwise (C2/C5: stream -18/-20 %) (tools/sweep35.txt)
+    // long traversals: C3 +6 %), the regenerating kernel otherwise (C2/C5: stream -18/-20 %) (tools/sweeps/sweep35.txt)
     const bool deep_blas = c->stack_depth > HG_DESCENT_DEEP + 2;
     const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (deep_blas ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
                                                      : c->kernel;
@@ -763,13 +782,13 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                            p.halogenDebugMode == 0 &&
                            kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
-        // tools/sweep12.txt), 256 for the lockstep one
+        // tools/sweeps/sweep12.txt), 256 for the lockstep one
         const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
         const int mblock = pool_k ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
         // about 6x (formerly 16x, 12x) as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
-        // (bit-identical).  Measured (tools/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
+        // (bit-identical).  Measured (tools/sweeps/sweep16-17.txt): C3 1080p 1180 -> 1251 Mpaths/s at N=1, and one
         // rank's share at N=8 314 -> 1212.
         const bool stream_k = regen && kern == HG_KERNEL_MEGA_STREAM;
         const int64_t tiles = c->n_local_tiles;
@@ -782,10 +801,17 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
             // about 6 launches' worth of wave slots: with the cost order and a tile's chunks on consecutive waves
             // (wave_unit), fewer, longer waves win: a rank's share at N=2 split 2 vs 4 -> 2,409 vs 2,308, N=8 8 vs 16
-            // -> 2,440 vs 2,337, C2 / C5 2 vs 3 -> +1.5 / +2.7 %, C3 at N=1 stays unsplit (tools/sweep82-83.txt;
+            // -> 2,440 vs 2,337, C2 / C5 2 vs 3 -> +1.5 / +2.7 %, C3 at N=1 stays unsplit (tools/sweeps/sweep82-83.txt;
             // the multiplier was 16, then 12 with the chunk-major cost order)
             else split = int(std::min<int64_t>(n_frames, (6 * resident + units - 1) / units));
         }
+        // the AQL dispatch packet's grid size is a 32-bit count of work-items: at most 2^26 - 1 waves of 64 lanes
+        constexpr int64_t kMaxWaves = (int64_t(1) << 26) - 1;
+        if (units > kMaxWaves) {
+            c->free_events.push_back(ev);
+            return fail(c, HG_E_UNSUPPORTED, "target too large: %lld work units", (long long)units);
+        }
+        if (units > 0) split = int(std::min<int64_t>(split, kMaxWaves / units));
         int chunk_max = HG_REGEN_MAX_CHUNK;
         if (split > 1) {
             const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
@@ -841,7 +867,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             kc.tile_order = nullptr;
             if (c->tile_order_on && tiles > 0 && !pool_k) {
                 const size_t tb = size_t(tiles) * sizeof(uint32_t);
-                if (int rc = ensure(c, c->tile_cost, tb)) {
+                if (int rc = ensure(c, c->tile_cost, 2 * tb)) {
                     c->free_events.push_back(ev);
                     return rc;
                 }
@@ -849,7 +875,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     c->free_events.push_back(ev);
                     return rc;
                 }
-                kc.tile_cost = static_cast<uint32_t*>(c->tile_cost.p);
+                kc.tile_cost = static_cast<unsigned long long*>(c->tile_cost.p);
             }
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
@@ -861,7 +887,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                                                   uint32_t(tiles), c->stream);
                         kc.tile_order = static_cast<const uint32_t*>(c->tile_order.p);
                     } else {
-                        e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(uint32_t), c->stream);
+                        e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(unsigned long long), c->stream);
                     }
                     c->tile_cost_valid = e == hipSuccess;
                 }
@@ -983,7 +1009,7 @@ int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
     if (!c) return HG_E_INVALID;
     if (int rc = set_device(c)) return rc;
     if (test != HG_SELFTEST_RCP) return fail(c, HG_E_INVALID, "unknown self-test %d", test);
-    const int64_t r = hg_wf_selftest_rcp(tested);
+    const int64_t r = hg_selftest_rcp_all(tested);
     if (r < 0) return fail(c, HG_E_HIP, "self-test failed to run");
     return r;
 }
@@ -994,7 +1020,9 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_KERNEL:
             if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
                 value != HG_KERNEL_MEGA_STREAM && value != HG_KERNEL_MEGA_POOL && value != HG_KERNEL_AUTO)
-                return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built", value);
+                return fail(c, HG_E_INVALID, "unknown kernel variant %d", value);
+            if (!HG_WITH_VARIANTS && (value == HG_KERNEL_WAVEFRONT || value == HG_KERNEL_MEGA_POOL))
+                return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built (A/B variants: make VARIANTS=1)", value);
             c->kernel = value;
             return HG_OK;
         case HG_OPT_BLOCK:

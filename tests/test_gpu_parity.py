@@ -2,6 +2,7 @@
 oracle.  The bar is bit-exact float32 equality (stronger than the 1e-4 relative bound of BASELINE.json's
 north_star); integer work counters must match exactly."""
 import json
+import os
 from pathlib import Path
 
 import numpy as np
@@ -15,11 +16,13 @@ GOLD = Path(__file__).resolve().parent / "golden"
 REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a diagnostic, the test is bitwise
 
 
-KERNELS = {"wavefront": abi.HG_KERNEL_WAVEFRONT, "mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN,
-           "stream": abi.HG_KERNEL_MEGA_STREAM, "pool": abi.HG_KERNEL_MEGA_POOL, "auto": abi.HG_KERNEL_AUTO}
+KERNELS = {"mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
+           "auto": abi.HG_KERNEL_AUTO}
+if os.environ.get("HG_TEST_VARIANTS") == "1":  # library built with make VARIANTS=1 (the A/B kernels)
+    KERNELS.update({"wavefront": abi.HG_KERNEL_WAVEFRONT, "pool": abi.HG_KERNEL_MEGA_POOL})
 
 
-def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="wavefront",
+def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="auto",
                block=None):
     own = ctx is None
     ctx = ctx or abi.Context(0)

@@ -6,7 +6,7 @@ from halogen import abi
 
 @pytest.mark.gpu
 def test_fast_reciprocal_is_correctly_rounded(gpu):
-    """rcp_exact (hg_wavefront.hip): v_rcp_f32 + one FMA Newton step == IEEE 1.0f/x for all 2^32 bit patterns
+    """rcp_exact (hg_device.h; self-test kernel in hg_selftest.hip): v_rcp_f32 + one FMA Newton step == IEEE 1.0f/x for all 2^32 bit patterns
     whose exponent field is in [2, 252] (x and 1/x normal); the rest take the IEEE division."""
     with abi.Context(0) as ctx:
         bad, tested = ctx.selftest(abi.HG_SELFTEST_RCP)
