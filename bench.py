@@ -98,6 +98,10 @@ def main():
     ap.add_argument("--save-image", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
+    ap.add_argument("--gather", default="", choices=["", "abi", "torch"],
+                    help="N > 1: the final tile gather through the C-ABI (hg_comm, RCCL; default with --dist-backend "
+                         "nccl) or through torch.distributed (default with gloo: the one-GPU rehearsal, where RCCL "
+                         "refuses two ranks on one device)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
@@ -162,6 +166,12 @@ def main():
     ctx.resize(W, H)
     ctx.set_tiling(rank, emu or world)
     ctx.set_params(params)
+    comm = None
+    gather_mode = args.gather or ("abi" if args.dist_backend == "nccl" else "torch")
+    if dist is not None and gather_mode == "abi":  # hg_comm over RCCL: rank 0 makes the id, every rank joins
+        box = [abi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = abi.Comm.rank(ctx, world, box[0], rank)
     setup_s = time.perf_counter() - t_setup
 
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
@@ -186,7 +196,9 @@ def main():
     for _ in range(args.steps):
         ctx.render(frames_per_step, True)
     gathered = None
-    if dist is not None:
+    if comm is not None:
+        comm.gather(0)  # enqueued on the context stream after the renders; the barrier below waits for it
+    elif dist is not None:
         import torch
 
         from halogen import distributed as hd
@@ -197,6 +209,8 @@ def main():
         gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H)
     barrier()
     dt = time.perf_counter() - t0
+    if comm is not None and rank == 0:
+        gathered = comm.readback(W, H)
 
     timing = ctx.counters()  # kernel_ms / launches of the timed launches
     kernel_symbol = KERNEL_SYMBOL.get(int(timing["last_kernel"]), "?")  # the variant HG_KERNEL_AUTO resolved to
@@ -295,18 +309,23 @@ def main():
             "emulated_ranks": emu or None,
             # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
             "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,
+            "gather": (gather_mode + (f" (hg_comm transport {comm.transport})" if comm is not None else ""))
+            if dist is not None else None,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},
             "cpu_baseline": None,
         }
         if args.save_image:
-            img = gathered.cpu().numpy() if gathered is not None else timed_img
+            img = (gathered if isinstance(gathered, np.ndarray) else gathered.cpu().numpy()) if gathered is not None \
+                else timed_img
             np.save(args.save_image, img)
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
             result["cpu_baseline"] = cpu_baseline(packed, params, cube, W, H, args.cpu_seconds, threads)
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.close()
     ctx.close()
     if dist is not None:
         dist.barrier()

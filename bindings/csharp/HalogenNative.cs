@@ -68,6 +68,7 @@ public static class HalogenNative
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8;
     public const int HG_SELFTEST_RCP = 1;
+    public const int HG_COMM_ID_BYTES = 128, HG_COMM_RCCL = 1, HG_COMM_PEER = 2;
 
     [DllImport(Lib)] public static extern int hg_abi_version();
     [DllImport(Lib)] public static extern int hg_create(int device, out IntPtr ctx);
@@ -101,6 +102,18 @@ public static class HalogenNative
         [Out] float[] outMin, [Out] float[] outMax);
     [DllImport(Lib)] public static extern int hg_pack_triangles(float[] vertices, float[] normals, int nVertices,
         int[] indices, int nTris, [Out] HalogenTriangle[] outTriangles);
+
+    // Multi-GPU gather (one context per GPU; the render pass keeps one HalogenRenderPass per device and gathers the
+    // tiles to the display device once per displayed image).
+    [DllImport(Lib)] public static extern int hg_comm_unique_id([Out] byte[] id);
+    [DllImport(Lib)] public static extern int hg_comm_init_rank(IntPtr ctx, int nRanks, byte[] id, int rank,
+        out IntPtr comm);
+    [DllImport(Lib)] public static extern int hg_comm_init_all(IntPtr[] ctxs, int nRanks, out IntPtr comm);
+    [DllImport(Lib)] public static extern int hg_comm_gather(IntPtr comm, int root);
+    [DllImport(Lib)] public static extern int hg_comm_readback(IntPtr comm, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_comm_transport(IntPtr comm);
+    [DllImport(Lib)] public static extern IntPtr hg_comm_last_error(IntPtr comm);
+    [DllImport(Lib)] public static extern void hg_comm_destroy(IntPtr comm);
 
     public static void Check(IntPtr ctx, int rc, string what)
     {

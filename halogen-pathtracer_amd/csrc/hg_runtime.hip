@@ -18,6 +18,7 @@
 #include "halogen_abi.h"
 #include "hg_fmath.h"
 #include "hg_layout.h"
+#include "hg_ctx.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
@@ -51,62 +52,7 @@ namespace {
 constexpr size_t kFrameColorCap = size_t(4) << 30;  // frame-parallel colour buffer cap (bytes)
 constexpr uint32_t kMaxStack = 64;  // LDS stack entries per lane; BLAS depth must be <= kMaxStack - 2
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-};
-
 }  // namespace
-
-struct hg_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-
-    // scene
-    bool has_scene = false;
-    DevBuf spheres, meshes, materials, nodes, leaves, tri_a, tri_b, tri_c, normals;
-    int32_t n_spheres = 0, n_meshes = 0, n_materials = 0, n_tris = 0, n_nodes = 0;
-    uint32_t stack_depth = 2;
-
-    // cubemap
-    DevBuf cube;
-    int32_t cube_size = 0, cube_mips = 0;
-    uint32_t cube_mip_offset[HG_MAX_CUBE_MIPS] = {};
-
-    // params
-    bool has_params = false;
-    hg_params params{};
-
-    // target
-    int32_t W = 0, H = 0, rank = 0, n_ranks = 1, tiles_x = 0, tiles_y = 0, n_local_tiles = 0;
-    DevBuf acc;
-
-    // wavefront pipeline state (hg_wavefront.hip), sized for the local pixel slots
-    DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
-    DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
-    DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
-    DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
-    DevBuf pool;                 // path-pool kernel: per-wave path slots
-    DevBuf cam_a, cam_b;         // camera-ray pass: primary rays of this launch chunk
-    DevBuf tile_cost, tile_order;  // cost-ordered dispatch: per local tile, wave-clock cost / dispatch order
-    bool tile_cost_valid = false;  // tile_cost holds the previous regen/stream launch's costs for this tiling
-    uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
-    size_t poll_cap = 0;
-    std::vector<hipEvent_t> poll_events;
-
-    // counters / timing
-    DevBuf counters_dev;
-    hg_counters counters{};
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events, pending_trace;
-
-    // device / options
-    int n_cu = 0;
-    int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0, refill = 32;
-    int32_t frame_split = 0;  // 0: automatic (see hg_render)
-    int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
-    int32_t tile_order_on = HG_TILE_ORDER;  // HG_OPT_TILE_ORDER
-};
 
 namespace {
 

@@ -101,7 +101,11 @@ EXPORTS = [
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
     "hg_readback", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
     "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
+    "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_readback",
+    "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
 ]
+HG_COMM_ID_BYTES = 128
+HG_COMM_RCCL, HG_COMM_PEER = 1, 2
 HG_SELFTEST_RCP = 1
 
 _lib = None
@@ -141,6 +145,14 @@ def lib() -> C.CDLL:
         "hg_build_blas_mt": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64, i32]),
         "hg_unity_bounds": (None, [f32p, f32p, i32, f32p, f32p]),
         "hg_pack_triangles": (C.c_int, [P, P, i32, P, i32, P]),
+        "hg_comm_unique_id": (C.c_int, [C.c_char_p]),
+        "hg_comm_init_rank": (C.c_int, [P, i32, C.c_char_p, i32, C.POINTER(P)]),
+        "hg_comm_init_all": (C.c_int, [C.POINTER(P), i32, C.POINTER(P)]),
+        "hg_comm_gather": (C.c_int, [P, i32]),
+        "hg_comm_readback": (C.c_int, [P, f32p, sz]),
+        "hg_comm_transport": (C.c_int, [P]),
+        "hg_comm_last_error": (C.c_char_p, [P]),
+        "hg_comm_destroy": (None, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -260,6 +272,80 @@ class Context:
         if r < 0:
             self._check(int(r), "hg_selftest")
         return int(r), int(tested.value)
+
+
+def comm_unique_id() -> bytes:
+    """A fresh communicator id (hg_comm_unique_id): made once by the root process and sent to every rank."""
+    buf = C.create_string_buffer(HG_COMM_ID_BYTES)
+    rc = lib().hg_comm_unique_id(buf)
+    if rc != HG_OK:
+        raise HalogenError(f"hg_comm_unique_id failed ({rc})")
+    return buf.raw
+
+
+class Comm:
+    """hg_comm: the multi-GPU gather of the ranks' tiles to a root.  Comm.rank(ctx, n, id, r) joins
+    one process's rank (one process per GPU); Comm.all(ctxs) covers every rank of this process.  Destroy it (close)
+    before its contexts."""
+
+    def __init__(self, handle: C.c_void_p, ctxs):
+        self._h = handle
+        self._ctxs = list(ctxs)  # kept alive while the comm exists
+
+    @classmethod
+    def rank(cls, ctx: "Context", n_ranks: int, uid: bytes, rank: int) -> "Comm":
+        h = C.c_void_p()
+        rc = lib().hg_comm_init_rank(ctx._h, n_ranks, uid, rank, C.byref(h))
+        if rc != HG_OK:
+            msg = lib().hg_last_error(ctx._h)
+            raise HalogenError(f"hg_comm_init_rank failed ({rc}): {msg.decode() if msg else ''}")
+        return cls(h, [ctx])
+
+    @classmethod
+    def all(cls, ctxs) -> "Comm":
+        arr = (C.c_void_p * len(ctxs))(*[c._h for c in ctxs])
+        h = C.c_void_p()
+        rc = lib().hg_comm_init_all(arr, len(ctxs), C.byref(h))
+        if rc != HG_OK:
+            msg = lib().hg_last_error(ctxs[0]._h)
+            raise HalogenError(f"hg_comm_init_all failed ({rc}): {msg.decode() if msg else ''}")
+        return cls(h, ctxs)
+
+    def _check(self, rc: int, what: str):
+        if rc != HG_OK:
+            msg = lib().hg_comm_last_error(self._h)
+            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    @property
+    def transport(self) -> int:
+        return int(lib().hg_comm_transport(self._h))
+
+    def gather(self, root: int = 0) -> None:
+        self._check(lib().hg_comm_gather(self._h, root), "hg_comm_gather")
+
+    def readback(self, w: int, h: int, out: np.ndarray | None = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros((h, w, 4), dtype=np.float32)
+        self._check(lib().hg_comm_readback(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size),
+                    "hg_comm_readback")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().hg_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def gpu_available() -> bool:

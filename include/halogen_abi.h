@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 1
+#define HG_ABI_VERSION 2
 
 /* ----------------------------------------------------------------------------------------------
  * Reference host structs (byte-identical to the C# [Sequential] structs)
@@ -165,7 +165,8 @@ enum {
     HG_E_NOMEM = -3,
     HG_E_NOSCENE = -4,
     HG_E_NOTARGET = -5,  /* hg_resize not called */
-    HG_E_UNSUPPORTED = -6
+    HG_E_UNSUPPORTED = -6,
+    HG_E_COMM = -7       /* RCCL error (text from ncclGetErrorString) or a mismatched communicator */
 };
 
 /* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v); all produce bit-identical images.
@@ -241,7 +242,9 @@ int hg_synchronize(hg_ctx* ctx);
 int hg_readback(hg_ctx* ctx, float* rgba, size_t n_floats);
 
 /* Device-to-device copy of this rank's packed tiles (n_local_tiles * 64 * 4 floats, tile-major,
- * pixel (lx,ly) of a tile at lx + 8*ly) into caller-owned device memory on the same device. */
+ * pixel (lx,ly) of a tile at lx + 8*ly) into caller-owned device memory on the same device.  Returns after the copy
+ * has completed on the context stream; a consumer on another stream or engine must order itself after the call.
+ * (The multi-GPU path uses hg_comm_gather instead, which stays on the contexts' own streams.) */
 int hg_copy_tiles_device(hg_ctx* ctx, void* dst_device, size_t n_bytes);
 int32_t hg_local_tile_count(const hg_ctx* ctx);
 
@@ -256,6 +259,42 @@ int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
  * or a negative error; *tested (optional) receives the number of inputs checked. */
 enum { HG_SELFTEST_RCP = 1 };
 int64_t hg_selftest(hg_ctx* ctx, int32_t test, int64_t* tested);
+
+/* ----------------------------------------------------------------------------------------------
+ * Multi-GPU framebuffer gather (not in the reference, which is single-GPU).
+ * Every rank renders the 8x8 tiles t % n_ranks == rank of the same image (hg_set_tiling) with its own context, on
+ * its own GPU; the only exchange is one gather of the ranks' accumulated tiles to the root, which assembles the
+ * row-major image on its device.  Two ways to build the communicator over the rank contexts:
+ *   hg_comm_init_rank  one process per GPU (e.g. under torchrun, MPI, or any launcher): rank 0 makes an id with
+ *                      hg_comm_unique_id, the caller distributes it, every rank joins (blocks until all have);
+ *   hg_comm_init_all   one process driving all the contexts (e.g. the C# render pass with one context per GPU,
+ *                      one host thread per device for hg_render): a single call over all contexts.
+ * Transport: RCCL point-to-point over xGMI (ncclSend / ncclRecv on each context's own stream, so the gather is
+ * ordered after that context's renders with no host wait).  hg_comm_init_all over contexts that share a device
+ * (a one-GPU rehearsal; RCCL refuses two ranks on one GPU) uses in-process device copies instead, ordered by events.
+ * The comm does not own the contexts; destroy it before them.  Not thread-safe.
+ * -------------------------------------------------------------------------------------------- */
+typedef struct hg_comm hg_comm;
+#define HG_COMM_ID_BYTES 128   /* = NCCL_UNIQUE_ID_BYTES */
+enum { HG_COMM_RCCL = 1, HG_COMM_PEER = 2 };
+
+/* A fresh communicator id (ncclGetUniqueId): made once, by the root process, and handed to every rank. */
+int hg_comm_unique_id(uint8_t id[HG_COMM_ID_BYTES]);
+/* This process's rank of an n_ranks communicator; ctx must already be tiled as (rank, n_ranks). Blocks until every
+ * rank has joined. */
+int hg_comm_init_rank(hg_ctx* ctx, int32_t n_ranks, const uint8_t id[HG_COMM_ID_BYTES], int32_t rank,
+                      hg_comm** out);
+/* All ranks in this process: ctxs[r] is rank r of n_ranks (each already tiled as (r, n_ranks)). */
+int hg_comm_init_all(hg_ctx* const* ctxs, int32_t n_ranks, hg_comm** out);
+/* Collective (every rank calls it; with hg_comm_init_all one call covers all ranks): gather the ranks' accumulated
+ * tiles to `root`, which assembles the full row-major RGBA32F image on its device.  Asynchronous on the contexts'
+ * streams.  All ranks must have the same target size. */
+int hg_comm_gather(hg_comm* comm, int32_t root);
+/* On the process holding the root (after hg_comm_gather): the assembled image, width*height*4 floats. Blocks. */
+int hg_comm_readback(hg_comm* comm, float* rgba, size_t n_floats);
+int hg_comm_transport(const hg_comm* comm);     /* HG_COMM_RCCL or HG_COMM_PEER */
+const char* hg_comm_last_error(const hg_comm* comm);
+void hg_comm_destroy(hg_comm* comm);
 
 /* ----------------------------------------------------------------------------------------------
  * Host-side data producers (the reference keeps these in C#: BVHGenerator.cs, RayTracingMesh.cs,
