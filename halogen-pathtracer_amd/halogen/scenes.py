@@ -21,44 +21,49 @@ from .unity import Transform, euler_to_quat, unity_cube, unity_plane
 
 ASSETS = Path(__file__).resolve().parents[2] / "assets"
 
-CORNELL_ROOT = (3.48, 1.24, 1.55)  # Testing Scene.unity:2378
+# Constants of the "Cornell Box" subtree of Testing Scene.unity, exactly as the file writes them (float32 shortest
+# round-trip decimals, -0 kept), pinned by tests/test_scene_constants.py against tests/golden/unity_scene.json
+# (tools/extract_unity_scene.py parses the reference files into that fixture).
+CORNELL_ROOT = (3.48, 1.24, 1.55)  # Testing Scene.unity:2378 (rotation identity, scale 1)
 
 WHITE = HalogenMaterial.default((1.0, 1.0, 1.0, 1.0))
-CYAN = HalogenMaterial.default((0.0, 0.8414836, 1.0, 1.0))        # Plane (2), :544
-RED = HalogenMaterial.default((1.0, 0.27699995, 0.27699995, 1.0))  # Plane (3), :874
+CYAN = HalogenMaterial(color=(0.0, 0.8414836, 1.0, 1.0))         # Plane (2), :544
+RED = HalogenMaterial(color=(1.0, 0.27699995, 0.27699995, 1.0))  # Plane (3), :874
 LIGHT = HalogenMaterial(color=(1, 1, 1, 1), specularColor=(1, 1, 1, 1), subsurfaceColor=(1, 1, 1, 1),
                         emissionColor=(1, 1, 1, 1), emissionIntensity=5.0)  # Light, :1566-1588
 CUBE1 = HalogenMaterial(color=(1, 1, 1, 1), specularColor=(1, 1, 1, 1),
                         subsurfaceColor=(1.0, 0.13679248, 0.13679248, 1.0), indexOfRefraction=1.1)  # Cube (1), :9333
-DRAGON = HalogenMaterial(color=(0.4716981, 0.4716981, 0.4716981, 1.0), metallic=0.5)  # Dragon_87k instance
+DRAGON = HalogenMaterial(color=(0.4716981, 0.4716981, 0.4716981, 1.0), metallic=0.5)  # Dragon_87k instance, :814-823
 DIFFUSE_SPHERE = HalogenMaterial.default((0.2, 0.75, 0.3, 1.0))
 GLASS_SPHERE = HalogenMaterial(color=(1.0, 1.0, 1.0, 0.05), roughness=0.05, metallic=0.02,
                                subsurfaceColor=(1.0, 0.55, 0.55, 1.0), indexOfRefraction=1.5, absorption=0.3)
 
+# (name, built-in mesh, local position, local rotation (x, y, z, w), local scale, material); children of the root
+CORNELL_WALLS = [
+    ("Plane", "Plane", (0, -2.5, 16), (0, 0, 0, 1), (0.5, 1, 0.5), WHITE),
+    ("Plane (4)", "Plane", (0, 2.5, 16), (0, 0, 1, 0), (0.5, 1, 0.5), WHITE),
+    ("Plane (1)", "Plane", (0, 0, 18.5), (-0.7071068, 0, 0, 0.7071068), (0.5, 1, 0.5), WHITE),
+    ("Plane (2)", "Plane", (2.5, 0, 16), (-0.5, 0.5, 0.5, 0.5), (0.5, 1, 0.5), CYAN),
+    ("Plane (3)", "Plane", (-2.5, 0, 16), (-0.5, -0.5, -0.5, 0.5), (0.5, 1, 0.5), RED),
+]
+CORNELL_LIGHT = ("Light", "Cube", (0, 2.47, 16.24), (0, 0, 0, 1), (1.5, 0.25, 1.5), LIGHT)
+CORNELL_FRONT_PANEL_ACTIVE = False  # "Front Panel" (z 13.5) is inactive in the scene: the box is open
+# children of "Basic Interior" (identity transform under the root)
+CORNELL_INTERIOR = [
+    ("Cube", "Cube", (-1.1599998, -1.25, 16.83), (-0.0, -0.14046915, -0.0, 0.99008507), (1.4999999, 2.5, 1.4999999),
+     WHITE),
+    ("Cube (1)", "Cube", (0.91, -1.53, 15.85), (-0.0, 0.2588186, -0.0, 0.965926), (1.5, 1.5, 1.5), CUBE1),
+    ("Cube (3)", "Cube", (-0.7750001, -2.37, 14.860999), (-0.0, 0.115712814, -0.0, 0.99328274), (1.2, 0.25, 1.2),
+     WHITE),
+]
+
 
 def _cornell_shell(scene: Scene, root: Transform, with_interior: bool):
-    pv, pn, pt = unity_plane()
-    cv, cn, ct = unity_cube()
-    half = (0.5, 1.0, 0.5)
-    walls = [  # (name, local pos, quaternion, material)  Testing Scene.unity Appendix B of SURVEY.md
-        ("Plane", (0, -2.5, 16), (0, 0, 0, 1), WHITE),
-        ("Plane (1)", (0, 0, 18.5), (-0.7071068, 0, 0, 0.7071068), WHITE),
-        ("Plane (2)", (2.5, 0, 16), (-0.5, 0.5, 0.5, 0.5), CYAN),
-        ("Plane (3)", (-2.5, 0, 16), (-0.5, -0.5, -0.5, 0.5), RED),
-        ("Plane (4)", (0, 2.5, 16), (0, 0, 1, 0), WHITE),
-    ]
-    for name, pos, q, mat in walls:
-        scene.add(RayTracingMesh(name, pv, pn, pt, Transform(pos, q, half, root), mat))
-    scene.add(RayTracingMesh("Light", cv, cn, ct, Transform((0, 2.47, 16.24), (0, 0, 0, 1), (1.5, 0.25, 1.5), root),
-                             LIGHT))
-    if with_interior:
-        scene.add(RayTracingMesh("Cube", cv, cn, ct,
-                                 Transform((-1.16, -1.25, 16.83), (0, -0.1405, 0, 0.9901), (1.5, 2.5, 1.5), root), WHITE))
-        scene.add(RayTracingMesh("Cube (1)", cv, cn, ct,
-                                 Transform((0.91, -1.53, 15.85), (0, 0.2588, 0, 0.9659), (1.5, 1.5, 1.5), root), CUBE1))
-        scene.add(RayTracingMesh("Cube (3)", cv, cn, ct,
-                                 Transform((-0.775, -2.37, 14.861), (0, 0.1157, 0, 0.9933), (1.2, 0.25, 1.2), root),
-                                 WHITE))
+    meshes = {"Plane": unity_plane(), "Cube": unity_cube()}
+    objects = CORNELL_WALLS + [CORNELL_LIGHT] + (CORNELL_INTERIOR if with_interior else [])
+    for name, mesh, pos, q, scale, mat in objects:
+        v, n, t = meshes[mesh]
+        scene.add(RayTracingMesh(name, v, n, t, Transform(pos, q, scale, root), mat))
 
 
 def cornell_box() -> Scene:

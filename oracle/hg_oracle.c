@@ -375,6 +375,27 @@ static void scene_isect_spheres(tstate* t, const ray_t* ray, hit_t* closest) {
 }
 
 #define NODE_STACK 64 /* reference: int NodeStack[32] (:397); 33 can be needed at depth cap 32, see DESIGN.md */
+#define REF_NODE_STACK 32 /* the reference's array size: a push at index >= 32 is out of bounds in HC:397-444 */
+
+/* Diagnostics (test infra): mesh traversals whose stack would outgrow the reference's NodeStack[32], and the
+ * deepest stack seen, since the last hgo_stack_stats(reset=1). */
+static _Atomic uint64_t g_stack_overflow_traversals;
+static _Atomic int32_t g_stack_max;
+void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t reset) {
+    if (overflow_traversals) *overflow_traversals = g_stack_overflow_traversals;
+    if (max_depth) *max_depth = g_stack_max;
+    if (reset) {
+        g_stack_overflow_traversals = 0;
+        g_stack_max = 0;
+    }
+}
+static void note_stack(int high) {
+    if (high > REF_NODE_STACK) g_stack_overflow_traversals++;
+    int32_t cur = g_stack_max;
+    while (high > cur && !__atomic_compare_exchange_n((int32_t*)&g_stack_max, &cur, high, 0, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED)) {
+    }
+}
 
 /* get_ray_scene_intersection_mesh, :378-472 */
 static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
@@ -393,9 +414,10 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
         ray_t pre = local;
         pre.d = v3(1.0f / local.d.x, 1.0f / local.d.y, 1.0f / local.d.z);
         uint32_t stack[NODE_STACK];
-        int sp = 0;
+        int sp = 0, high = 1;
         stack[sp++] = md->accelerationBufferOffset;
         while (sp > 0) {
+            if (sp > high) high = sp;
             const BVHEntry* node = &sc->blas[stack[--sp]];
             if (node->triangleCount > 0) {
                 for (uint32_t k = 0; k < node->triangleCount; k++) {
@@ -427,6 +449,7 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
                 }
             }
         }
+        note_stack(high);
     }
     if (closest.rayT < (closestHit->rayT - eps) && closest.rayT < t->p->viewParameters.w) {
         const HalogenMeshData* md = &sc->meshes[closest.mesh];

@@ -62,6 +62,10 @@ int hgo_render(const hgo_scene* scene, const hg_params* params, int32_t n_frames
 void hgo_trace_pixel(const hgo_scene* scene, const hg_params* params, uint32_t x, uint32_t y, int32_t frame,
                      float rgb[3], hg_counters* counters);
 
+/* Diagnostics: mesh traversals (since the last reset) whose node stack would hold more than the reference's
+ * NodeStack[32] entries (HC:397), and the deepest stack seen. */
+void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t reset);
+
 /* Per-stage KAT entry points */
 float hgo_sphere_t(const float o[3], const float d[3], const float c[3], float r);
 float hgo_triangle_t(const float o[3], const float d[3], const float v0[3], const float v1[3], const float v2[3],

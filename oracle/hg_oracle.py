@@ -71,6 +71,8 @@ def lib():
         L.hgo_triangle_t.argtypes = [fp, fp, fp, fp, fp, fp, fp, fp]
         L.hgo_aabb_t.restype = C.c_float
         L.hgo_aabb_t.argtypes = [fp, fp, fp, fp]
+        L.hgo_stack_stats.restype = None
+        L.hgo_stack_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_int32), C.c_int32]
         L.hgo_cube_sample.restype = None
         L.hgo_cube_sample.argtypes = [C.POINTER(HgoScene), fp, C.c_int32, fp]
         _lib = L
@@ -119,3 +121,10 @@ def render(packed, params, n_frames: int, accumulate: bool = True, acc: np.ndarr
         raise RuntimeError(f"hgo_render failed: {rc}")
     del keep
     return acc, cnt.as_dict()
+
+
+def stack_stats(reset: bool = False) -> tuple[int, int]:
+    """(mesh traversals whose node stack outgrew the reference's NodeStack[32], deepest stack) since the last reset."""
+    n, d = C.c_uint64(0), C.c_int32(0)
+    lib().hgo_stack_stats(C.byref(n), C.byref(d), 1 if reset else 0)
+    return int(n.value), int(d.value)

@@ -23,6 +23,10 @@ CASES = {
     "c1_32_aperture": ("C1", 32, 32, 2, True, {"ApertureAngle": 2.0, "FocalPlaneDistance": 7.0, "FilterRadius": 1.5}),
     "glass_64x36": ("C5", 64, 36, 2, True, {}),
     "dragon1_64x36": ("C3", 64, 36, 2, True, {"_subdiv": 1}),
+    # the full 871,200-triangle dragon (C3's scene), 32-level BLAS: streaming kernel, distributed leaf test
+    "dragon10_64x36": ("C3", 64, 36, 16, True, {}),  # 16 frames: at 1 spp most Cornell paths end black
+    "dragon10_96x54_normal": ("C3", 96, 54, 1, True, {"DebugMode": "Normal"}),  # every dragon hit's normal
+    "dragon10_48x27_tritests": ("C3", 48, 27, 1, True, {"DebugMode": "RayTriangleTests", "FirstInteractionOnly": False}),
 }
 
 

@@ -76,3 +76,19 @@ def test_stage_kats(built):
     assert L.hgo_aabb_t(_f3(-1, -1, -1), _f3(1, 1, 1), _f3(0, 0, -5), _f3(inf, inf, 1)) == 4.0
     assert L.hgo_aabb_t(_f3(-1, -1, -1), _f3(1, 1, 1), _f3(0, 0, 0), _f3(inf, inf, 1)) == -1.0
     assert L.hgo_aabb_t(_f3(-1, -1, -1), _f3(1, 1, 1), _f3(3, 0, -5), _f3(inf, inf, 1)) == inf
+
+
+def test_reference_node_stack_never_overflows_c3(built):
+    """The reference's BLAS stack is `int NodeStack[32]` (HC:397); 33 entries are possible in principle at the
+    depth cap.  A band of the full C3 image (871k-triangle dragon) never needs more than 32 (the
+    deepest over 16 full frames is 23), so the oracle's and the kernel's deeper stacks change no result there."""
+    from halogen import render_pass as rp, scenes
+    cfg = scenes.CONFIGS["C3"]
+    s = rp.clamp_settings(scenes.settings_for(cfg))
+    packed = cases._scene("dragon", 10)
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), False)
+    hg_oracle.stack_stats(reset=True)
+    _, cnt = hg_oracle.render(packed, params, 1, True, pix_range=(400 * cfg.width, 700 * cfg.width))
+    over, deepest = hg_oracle.stack_stats(reset=True)
+    assert cnt["rays"] > 500_000
+    assert over == 0 and 8 <= deepest <= 32, (over, deepest)

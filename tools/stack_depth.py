@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""How often does the reference's traversal outgrow its `int NodeStack[32]` (HalgoenCompute.compute:397)?
+
+The oracle follows the reference's push order exactly (pop a node; inner node: push the farther child, then the
+nearer, each only if its box is entered before the closest hit) with a 64-entry stack, and records per mesh
+traversal the stack's high-water mark.  A traversal whose stack would hold 33 entries writes NodeStack[32] in the
+reference: out of bounds.  Usage: python tools/stack_depth.py [--config C3] [--frames 2] [--rows y0:y1]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "halogen-pathtracer_amd"), str(ROOT / "oracle"), str(ROOT / "tests")]
+
+import hg_oracle  # noqa: E402  (test infra: a diagnostic of the reference's behaviour, not a product path)
+from halogen import render_pass as rp, scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C3")
+ap.add_argument("--frames", type=int, default=2)
+ap.add_argument("--rows", default="")
+args = ap.parse_args()
+cfg = scenes.CONFIGS[args.config]
+settings = scenes.settings_for(cfg)
+s = rp.clamp_settings(settings)
+packed = cfg.build_scene().pack()
+cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
+params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
+W, H = cfg.width, cfg.height
+y0, y1 = (int(v) for v in args.rows.split(":")) if args.rows else (0, H)
+hg_oracle.stack_stats(reset=True)
+t0 = time.time()
+_, cnt = hg_oracle.render(packed, params, args.frames, True, cubemap=cube, pix_range=(y0 * W, y1 * W))
+over, deepest = hg_oracle.stack_stats()
+print(json.dumps({"config": args.config, "width": W, "rows": [y0, y1], "frames": args.frames,
+                  "paths": cnt["paths"], "rays": cnt["rays"], "mesh_traversals": cnt["mesh_visits"],
+                  "traversals_over_32": over, "deepest_stack": deepest,
+                  "fraction_of_rays": over / max(cnt["rays"], 1), "seconds": round(time.time() - t0, 1)}))
