@@ -13,10 +13,15 @@ accumulated image is bit-identical to a 1-GPU render of N*64*K frames.  The time
 on both sides, max over ranks) covers K steps and, for N > 1, the final RCCL gather of the tiles to rank 0.
 Scene build/upload and BVH build are outside it (as in the reference meter, HalogenDebugUI.cs:37-56).
 
-value = W*H*N*K / time (Mpaths/s); Mrays/s counts get_ray_intersection calls (device counters).
-roofline: algorithmic bytes per trace launch (32 B per AABB test, 36 B per triangle test,
-64 B per mesh transform, 44 B per sphere test, 284 B per accepted hit, 48 B per pixel-frame) over the mean
-launch duration from HIP events on the launch stream, against 8 TB/s.
+value = W*H*N*K / time (Mpaths/s); Mrays/s counts get_ray_intersection calls (device counters); primary_miss_frac
+is the share of paths whose camera ray hits nothing (one-ray paths), and "framed" repeats C3 with the box opening
+filling the frame (almost no such paths).
+roofline: the trace kernel is bound by VALU issue and latency on a cache-resident scene, so "frac" is its VALU
+issue rate (SQ_INSTS_VALU per launch from the committed rocprofv3 pass of this workload, over the launch duration
+measured here with HIP events on the launch stream) against 1,024 SIMDs x 2.4 GHz / 2 cycles; the PMC-measured
+DRAM-side bytes ("traffic") against 8 TB/s and SURVEY.md §8d's logical bytes (32 B per AABB test, 36 B per
+triangle test, 64 B per mesh transform, 44 B per sphere test, 284 B per accepted hit, 48 B per pixel-frame)
+are reported beside it.
 cpu_baseline: the CPU oracle (oracle/hg_oracle.c, a scalar C restatement of the same kernel) on rank 0 at N=1,
 on a stratified sample of row bands of the same workload, threads = min(16, cpus).
 """
@@ -39,6 +44,9 @@ from halogen import render_pass as rp  # noqa: E402
 from halogen import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per SIMD every 2 cycles
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles"), in G wave-instructions/s
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
 KERNEL_SYMBOL = {abi.HG_KERNEL_MEGA_POOL: "hg_trace_pool_kernel", abi.HG_KERNEL_MEGA_STREAM: "hg_trace_stream_kernel",
                  abi.HG_KERNEL_MEGA_REGEN: "hg_trace_regen_kernel", abi.HG_KERNEL_MEGA: "hg_trace_kernel",
                  abi.HG_KERNEL_WAVEFRONT: "hg_wf_trace"}
@@ -48,6 +56,74 @@ METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GP
 def algorithmic_bytes(c: dict) -> float:
     return (32.0 * c["aabb_tests"] + 36.0 * c["tri_tests"] + 64.0 * c["mesh_visits"] + 44.0 * c["sphere_tests"]
             + 284.0 * c["hits"] + 48.0 * c["paths"])
+
+
+def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -> dict:
+    """C3F beside the headline: the same scene, settings and image size with the camera moved in until the box
+    opening fills the frame (scenes.CORNELL_FRAMED_CAMERA_POS), so nearly every path enters the box.  Warm-up launch,
+    `steps` timed steps (device sync on both sides), then one counting replay step for the path statistics."""
+    cfg = scenes.CONFIGS["C3F"].resized(W, H)
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), False)
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.render(frames_per_step, True)  # warm-up: records this view's tile costs for the cost order
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.render(frames_per_step, True)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.reset_counters()
+    ctx.set_option(abi.HG_OPT_COUNTERS, 1)
+    ctx.render(frames_per_step, True)
+    c = ctx.counters()
+    paths = W * H * frames_per_step * steps
+    return {"workload": cfg.name, "value": paths / dt / 1e6, "unit": "Mpaths/s", "steps": steps,
+            "ms_per_step": dt * 1e3 / steps, "mrays_per_s": c["rays"] / c["paths"] * paths / dt / 1e6,
+            "primary_miss_frac": c["primary_misses"] / c["paths"], "rays_per_path": c["rays"] / c["paths"],
+            "tri_tests_per_path": c["tri_tests"] / c["paths"], "camera_position": list(scenes.CORNELL_FRAMED_CAMERA_POS)}
+
+
+def library_sha256() -> str:
+    import hashlib
+
+    return hashlib.sha256(abi.LIB_PATH.read_bytes()).hexdigest()
+
+
+def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str) -> dict:
+    """The dominant kernel against what bounds it.  The trace kernel works on a cache-resident scene (C3: 90 MB,
+    inside the 256 MiB Infinity Cache) and is bound by VALU issue and latency, not HBM: `frac` is its VALU issue rate
+    (wave-level VALU instructions per launch, SQ_INSTS_VALU from the committed rocprofv3 pass of this workload and
+    build, over the launch time measured live with HIP events) against 1,024 SIMDs x 2.4 GHz / 2 cycles.
+    lane_util is the mean fraction of the 64 lanes active in those instructions, so frac x lane_util is the share of
+    the chip's fp32 lane-issue slots doing work.  HBM stays beside it: the PMC-measured DRAM-side bytes (traffic)
+    against 8 TB/s, and the §8(d) logical bytes."""
+    ok = mean_launch_s > 0
+    valu = pmc.get("valu_insts_per_launch")
+    achieved = valu / mean_launch_s / 1e9 if valu and ok else None
+    frac = achieved / VALU_PEAK_GINST if achieved else None
+    lane = pmc.get("valu_lane_util")
+    traffic = pmc.get("hbm_bytes_per_launch")
+    lib_sha = library_sha256()
+    return {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
+            "unit_note": "wave64 VALU instructions issued per second (peak = 1024 SIMDs x 2.4 GHz / 2 cycles)",
+            "frac": frac, "lane_util": lane, "useful_lane_frac": frac * lane if frac and lane else None,
+            "wait_any_frac": pmc.get("wait_any_frac"), "l2_hit_rate": pmc.get("l2_hit_rate"),
+            "traffic": traffic,
+            "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and ok else None,
+            "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS if traffic and ok else None,
+            "hbm_peak_gbs": HBM_PEAK_GBS,
+            "write_bytes_per_launch": pmc.get("write_bytes_per_launch"),
+            "logical_bytes_per_launch": logical_per_launch,
+            "logical_gbs": logical_per_launch / mean_launch_s / 1e9 if logical_per_launch and ok else None,
+            "mean_launch_ms": mean_launch_s * 1e3, "kernel": kernel_symbol,
+            "counters_from": pmc.get("summary"),
+            "counters_library_matches": (pmc.get("library_sha256") == lib_sha) if pmc.get("library_sha256") else None}
 
 
 def cpu_baseline(packed, params, cube, width, height, seconds, threads):
@@ -88,6 +164,7 @@ def main():
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-framed", action="store_true", help="skip the C3F (box opening fills the frame) measurement")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
@@ -236,7 +313,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        keys = ["paths", "rays", "tri_tests", "aabb_tests", "mesh_visits", "sphere_tests", "hits"]
+        keys = ["paths", "rays", "tri_tests", "aabb_tests", "mesh_visits", "sphere_tests", "hits", "primary_misses"]
         v = torch.tensor([float(cnt[k]) for k in keys], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(v)
         totals = dict(zip(keys, (int(x) for x in v.tolist())))
@@ -251,9 +328,10 @@ def main():
         launches = max(cnt["launches"], 1)
         mean_launch_s = cnt["kernel_ms"] / 1e3 / launches
         counters_ok = not args.no_counters and cnt["paths"] > 0
-        bytes_per_launch = algorithmic_bytes(cnt) / launches if counters_ok else None
-        achieved = bytes_per_launch / mean_launch_s / 1e9 if counters_ok and mean_launch_s > 0 else None
-        traffic = None
+        # §8(d)'s byte model: LOGICAL bytes per launch (every node / triangle / record read the algorithm makes,
+        # whether L1/L2/Infinity Cache or HBM serves it) — a work measure, not a bound on this cache-resident kernel
+        logical_per_launch = algorithmic_bytes(cnt) / launches if counters_ok else None
+        pmc = {}
         tfile = ROOT / "profiles" / "pmc_traffic.json"
         if tfile.exists():
             try:
@@ -261,9 +339,10 @@ def main():
                 if (t.get("config") == args.config and t.get("width") == W and t.get("height") == H
                         and t.get("frames_per_launch") == frames_per_step
                         and str(t.get("kernel", "")).startswith(kernel_symbol + "<false")):  # counter-free build
-                    traffic = t.get("hbm_bytes_per_launch")
+                    pmc = t
             except Exception:
-                traffic = None
+                pmc = {}
+        roofline = roofline_of(pmc, mean_launch_s, logical_per_launch, kernel_symbol)
         result = {
             "metric": METRIC,
             "value": total_paths / dt / 1e6,
@@ -282,17 +361,12 @@ def main():
                        "triangles": len(packed.triangles), "blas_nodes": len(packed.blas),
                        "parallelism": f"tiles{world}"},
             "mrays_per_s": totals["rays"] / dt / 1e6 if counters_ok else None,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         # the PMC-measured DRAM-side bytes per launch over the same launch time (the working set
-                         # is cache-resident, so this is far below the algorithmic figure)
-                         "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and mean_launch_s > 0 else None,
-                         "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS
-                         if traffic and mean_launch_s > 0 else None,
-                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_launch_ms": mean_launch_s * 1e3,
-                         "kernel": kernel_symbol},
+            "roofline": roofline,
             "counters_per_path": {k: totals[k] / max(totals["paths"], 1) for k in
                                   ("rays", "tri_tests", "aabb_tests", "hits")} if counters_ok else None,
+            # share of the paths whose camera ray hits nothing (from C3's camera ~54 % leave through the open front
+            # as one ray): Mpaths/s counts them as paths, Mrays/s counts their single ray
+            "primary_miss_frac": totals["primary_misses"] / max(totals["paths"], 1) if counters_ok else None,
             "counting_replay_bit_identical": replay_identical,
             "simd_utilisation": {"descent": cnt["aabb_tests"] / 2 / max(64 * cnt["node_rounds"], 1),
                                  "leaf": cnt["tri_tests"] / max(64 * cnt["tri_rounds"], 1),
@@ -320,6 +394,8 @@ def main():
             img = (gathered if isinstance(gathered, np.ndarray) else gathered.cpu().numpy()) if gathered is not None \
                 else timed_img
             np.save(args.save_image, img)
+        if world == 1 and not emu and args.config == "C3" and not args.no_counters and not args.no_framed:
+            result["framed"] = framed_measurement(ctx, packed, s, W, H, frames_per_step, max(2, args.steps // 4))
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
             result["cpu_baseline"] = cpu_baseline(packed, params, cube, W, H, args.cpu_seconds, threads)

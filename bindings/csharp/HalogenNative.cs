@@ -60,6 +60,7 @@ public static class HalogenNative
         public ulong shade_cycles;
         [MarshalAs(UnmanagedType.ByValArray, SizeConst = 4)] public ulong[] shade_detail;
         public ulong shade_rounds;
+        public ulong primary_misses;
     }
 
     public const int HG_OK = 0;

@@ -123,6 +123,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 struct Counters {
     uint32_t rays, tri, aabb, node_rounds, tri_rounds, hits;  // *_rounds: wave-level loop iterations (one lane counts)
     uint32_t shade_rounds;
+    uint32_t primary_miss;  // camera rays that hit nothing
 };
 // 1 in exactly one active lane (the lowest): summed over lanes, counts the wave-level executions of a code point
 // Wave clock (s_memtime) for the counting instantiations' phase split; volatile + memory clobber keep the
@@ -1218,6 +1219,7 @@ __device__ f3 trace_ray(const HgKernelParams& kp, Sampler& smp, MediumStack& ms,
             if (rr > contribution) break;
             thr = thr * rcp_exact(contribution);
         } else {
+            c.primary_miss += it == 0u;
             acc = acc + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             break;
         }

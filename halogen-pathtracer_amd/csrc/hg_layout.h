@@ -191,7 +191,8 @@ struct HgKernelParams {
     const float4* __restrict__ cube;
     // outputs
     float4* __restrict__ acc;
-    unsigned long long* __restrict__ counters;  // 7 x u64, order of hg_counters' first 7 fields
+    unsigned long long* __restrict__ counters;  // 32 x u64: 0-6 hg_counters' first 7 fields, 7-15 wave-level
+                                                // rounds / clocks, 16 primary misses (hg_runtime.hip hg_get_counters)
 
     // wavefront pipeline state (hg_wavefront.hip), SoA, one entry per local pixel slot
     // (slot = local_tile*64 + lane, the same index as the tile-major accumulation buffer)

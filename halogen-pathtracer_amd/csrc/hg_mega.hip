@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKe
     const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
     const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
     const bool active = local_tile < kp.n_local_tiles && px < kp.Wu && py < kp.Hu;
-    Counters c{0, 0, 0, 0, 0, 0};
+    Counters c{0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
     if (active) {
         const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x,
@@ -67,6 +67,8 @@ __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKe
             const uint32_t s = wave_sum(v[k]);
             if (lane == 0 && s) atomicAdd(kp.counters + k, (unsigned long long)s);
         }
+        const uint32_t pm = wave_sum(c.primary_miss);
+        if (lane == 0 && pm) atomicAdd(kp.counters + 16, (unsigned long long)pm);
     }
 }
 
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
         work = chunk < split && px < kp.Wu && py < kp.Hu && f_end > f_begin;
     }
-    Counters c{0, 0, 0, 0, 0, 0};
+    Counters c{0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
     uint32_t fs = f_begin << 16;  // frame index << 16 | sample index
     uint32_t bounce = 0;          // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
@@ -296,6 +298,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                                                                  ((bounce >> 16) & 0xFFu) > kp.max_trans);
                 }
             } else {  // :941
+                c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
             if (!alive) {
@@ -372,6 +375,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         }
         const uint32_t sr = wave_sum(c.shade_rounds);
         if (lane == 0 && sr) atomicAdd(kp.counters + 15, (unsigned long long)sr);
+        const uint32_t pm = wave_sum(c.primary_miss);
+        if (lane == 0 && pm) atomicAdd(kp.counters + 16, (unsigned long long)pm);
     }
 }
 
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
         work = chunk < split && px < kp.Wu && py < kp.Hu && f_end > f_begin;
     }
-    Counters c{0, 0, 0, 0, 0, 0};
+    Counters c{0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
     uint32_t fs = f_begin << 16;  // frame index << 16 | sample index
     uint32_t bounce = 0;          // diffuse | glossy << 8 | transmission << 16 | bounce index << 24
@@ -558,6 +563,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                                                                  ((bounce >> 16) & 0xFFu) > kp.max_trans);
                 }
             } else {  // :941
+                c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
 #if HG_PHASE_DETAIL == 1
@@ -648,6 +654,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         }
         const uint32_t sr = wave_sum(c.shade_rounds);
         if (lane == 0 && sr) atomicAdd(kp.counters + 15, (unsigned long long)sr);
+        const uint32_t pm = wave_sum(c.primary_miss);
+        if (lane == 0 && pm) atomicAdd(kp.counters + 16, (unsigned long long)pm);
     }
 }
 

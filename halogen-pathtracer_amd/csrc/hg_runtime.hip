@@ -341,11 +341,11 @@ int hg_create(int device, hg_ctx** out) {
     hg_ctx* c = new hg_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters_dev.p, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->counters_dev.p, 32 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return HG_E_HIP;
     }
-    c->counters_dev.bytes = 16 * sizeof(unsigned long long);
+    c->counters_dev.bytes = 32 * sizeof(unsigned long long);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         delete c;
@@ -922,7 +922,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     if (int rc = set_device(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (int rc = drain_events(c)) return rc;
-    unsigned long long v[16];
+    unsigned long long v[32];
     HG_HIP(c, hipMemcpy(v, c->counters_dev.p, sizeof v, hipMemcpyDeviceToHost));
     *out = c->counters;
     out->paths = v[0];
@@ -938,6 +938,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->shade_cycles = v[10];
     for (int k = 0; k < 4; ++k) out->shade_detail[k] = v[11 + k];
     out->shade_rounds = v[15];
+    out->primary_misses = v[16];
     return HG_OK;
 }
 

@@ -81,7 +81,7 @@ class HgCounters(C.Structure):
                 ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
                 ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64),
                 ("trace_cycles", C.c_uint64), ("shade_cycles", C.c_uint64),
-                ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64)]
+                ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)

@@ -147,11 +147,19 @@ def nested_glass() -> Scene:
 
 
 CORNELL_CAMERA_POS = (CORNELL_ROOT[0], CORNELL_ROOT[1], CORNELL_ROOT[2] + 8.7)
+# The same camera moved in until the 5 x 5 opening of the box (local z 13.5) fills a 16:9 frame: at a 60 degree
+# vertical FOV the frame is 2 d tan(30) * 16/9 = 2.053 d wide at distance d, so d = 5 / 2.053 = 2.436 puts the
+# opening's side edges at the frame's edges and every camera ray enters the box (bench.py "framed" measurement).
+CORNELL_FRAMED_CAMERA_POS = (CORNELL_ROOT[0], CORNELL_ROOT[1], CORNELL_ROOT[2] + 13.5 - 2.436)
 GLASS_CAMERA_POS = (0.0, 2.2, -6.5)
 
 
 def cornell_camera(w: int, h: int) -> Camera:
     return Camera(Transform(CORNELL_CAMERA_POS, (0, 0, 0, 1)), 60.0, w, h)
+
+
+def cornell_framed_camera(w: int, h: int) -> Camera:
+    return Camera(Transform(CORNELL_FRAMED_CAMERA_POS, (0, 0, 0, 1)), 60.0, w, h)
 
 
 def glass_camera(w: int, h: int) -> Camera:
@@ -167,12 +175,15 @@ class Config:
     frames: int
     settings: HalogenSettings
     gpus: int = 1
+    view: str = "front"  # "front": CORNELL_CAMERA; "framed": the box opening fills the frame
 
     def build_scene(self) -> Scene:
         return {"cornell": cornell_box, "dragon": dragon_cornell, "glass": nested_glass}[self.scene]()
 
     def camera(self) -> Camera:
-        return (glass_camera if self.scene == "glass" else cornell_camera)(self.width, self.height)
+        if self.scene == "glass":
+            return glass_camera(self.width, self.height)
+        return (cornell_framed_camera if self.view == "framed" else cornell_camera)(self.width, self.height)
 
     def resized(self, w: int, h: int, frames: int | None = None) -> "Config":
         return replace(self, width=w, height=h, frames=self.frames if frames is None else frames)
@@ -185,6 +196,9 @@ CONFIGS = {
                  replace(_BASE, MaxBounces=8, DiffuseBounces=8)),
     "C3": Config("C3 dragon-871k cornell 1080p 64spp 8 bounces", "dragon", 1920, 1080, 64,
                  replace(_BASE, MaxBounces=8, DiffuseBounces=8, GlossyBounces=8)),
+    # C3 seen from inside the opening (no primary misses): the cost of a traced path without the open-front share
+    "C3F": Config("C3 dragon-871k cornell 1080p 64spp 8 bounces, box opening filling the frame", "dragon", 1920, 1080,
+                  64, replace(_BASE, MaxBounces=8, DiffuseBounces=8, GlossyBounces=8), view="framed"),
     "C4": Config("C4 dragon-871k cornell 4K 256spp 8 bounces 8 GPUs", "dragon", 3840, 2160, 256,
                  replace(_BASE, MaxBounces=8, DiffuseBounces=8, GlossyBounces=8), gpus=8),
     "C5": Config("C5 nested glass + env cubemap 1080p 64spp 12 transmission bounces", "glass", 1920, 1080, 64,

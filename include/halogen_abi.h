@@ -154,6 +154,8 @@ typedef struct hg_counters {
                                  hit resolve / material + BSDF / path end + camera ray / next-ray setup; else 0 */
     uint64_t shade_rounds; /* regenerating / streaming megakernels: wave-level iterations of the shading code (SIMD
                               utilisation of shading = rays / (64 * shade_rounds)) */
+    uint64_t primary_misses; /* paths whose camera ray hits nothing (trace_ray's first iteration takes the miss branch,
+                                HC:941): a one-ray path; primary_misses / paths is the share of near-free paths */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;

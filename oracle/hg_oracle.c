@@ -684,6 +684,7 @@ static f3 trace_ray(tstate* t, ray_t ray) {
             if (rr > contribution) break;
             thr = muls(thr, 1.0f / contribution);
         } else {
+            if (it == 0) t->cnt.primary_misses++; /* the camera ray hit nothing (diagnostic, not in the reference) */
             acc = add3(acc, mul3(sample_sky(t, ray.d, sky_level(p, accRough)), thr));
             break;
         }
@@ -796,6 +797,7 @@ void hgo_trace_pixel(const hgo_scene* scene, const hg_params* params, uint32_t x
         counters->mesh_visits += t.cnt.mesh_visits;
         counters->sphere_tests += t.cnt.sphere_tests;
         counters->hits += t.cnt.hits;
+        counters->primary_misses += t.cnt.primary_misses;
     }
 }
 
@@ -872,6 +874,7 @@ int hgo_render(const hgo_scene* scene, const hg_params* params, int32_t n_frames
             counters->mesh_visits += jobs[i].cnt.mesh_visits;
             counters->sphere_tests += jobs[i].cnt.sphere_tests;
             counters->hits += jobs[i].cnt.hits;
+            counters->primary_misses += jobs[i].cnt.primary_misses;
         }
     }
     free(jobs);

@@ -95,14 +95,19 @@ def make_scene(packed, cubemap=None) -> tuple[HgoScene, list]:
     return s, keep
 
 
-class Counters(C.Structure):  # hg_counters layout
+class Counters(C.Structure):  # hg_counters layout (include/halogen_abi.h), complete: the oracle writes any field
     _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("aabb_tests", C.c_uint64), ("mesh_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("hits", C.c_uint64), ("kernel_ms", C.c_double), ("launches", C.c_uint64),
-                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64)]
+                ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
+                ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64), ("trace_cycles", C.c_uint64),
+                ("shade_cycles", C.c_uint64), ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64),
+                ("primary_misses", C.c_uint64)]
+    _oracle_fields = ("paths", "rays", "tri_tests", "aabb_tests", "mesh_visits", "sphere_tests", "hits",
+                      "kernel_ms", "launches", "trace_ms", "trace_launches", "primary_misses")
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        return {n: getattr(self, n) for n in self._oracle_fields}
 
 
 def render(packed, params, n_frames: int, accumulate: bool = True, acc: np.ndarray | None = None,

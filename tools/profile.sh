@@ -3,7 +3,7 @@
 # its own time limit; any failure ends the script.  Output: gpurun_out/prof/<tag>_*.
 set -u
 TAG=${TAG:-r01}
-ARGS=${BENCH_ARGS:---steps 16 --warmup 2 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 16 --warmup 2 --no-cpu-baseline --no-framed}
 OUT=$PWD/gpurun_out/prof
 mkdir -p "$OUT"
 export TMPDIR=/tmp
