@@ -1,11 +1,10 @@
 // HalogenNative.cs — P/Invoke binding of libhalogen_hip.so (include/halogen_abi.h) for the reference's C# host.
 //
-// Drop next to Assets/Scripts/Render Features/HalogenRenderPass.cs.  The scene structs (HalogenSphere,
-// HalogenMeshData, PackedHalogenMaterial, HalogenTriangle, BVHEntry) are the reference's own
-// [StructLayout(LayoutKind.Sequential)] structs (HalogenRenderPass.cs:10-76) and are passed unchanged; only the
-// uniform block and the counters are new.  INTEGRATION.md §2 lists the call-site changes in HalogenRenderPass.
-// tests/test_csharp_binding.py checks this file against the C header (every export declared, struct fields in
-// order with matching types).  There is no C# toolchain in the build image, so it is not compiled here.
+// Used by HalogenRenderPass.cs of this directory, the drop-in for Assets/Scripts/Render Features/
+// HalogenRenderPass.cs.  The scene records (HalogenSphere, HalogenMeshData, PackedHalogenMaterial, HalogenTriangle,
+// BVHEntry) are declared in HalogenStructs.cs with the header's layout; only the uniform block and the counters are
+// new here.  tests/test_csharp_binding.py checks this file against the C header (every export declared, struct
+// fields in order with matching types); there is no C# toolchain in the build image, so it is not compiled here.
 using System;
 using System.Runtime.InteropServices;
 using UnityEngine;

@@ -965,8 +965,38 @@ __device__ __forceinline__ Hit trav_hit(const HgKernelParams& kp, const Ray& ray
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Sky (:196-204) — manual bilinear cubemap, the build's definition of SampleLevel
+// Sky (:196-204): TextureCube.SampleLevel (HC:201) with an integral level = bilinear within one mip, seamless across
+// faces as D3D10+ filters cube maps (resting_place_4k.exr.meta:32 imports it seamless): a footprint texel beyond a
+// face edge is read from the adjacent face, and at a cube corner the missing fourth texel is the average of the
+// three that exist.  The same integer adjacency and operation order as the oracle (oracle/hg_oracle.c).
 // ---------------------------------------------------------------------------------------------------
+// face frames: major axis M, s axis S, t axis T (sc = dot(d, S), tc = dot(d, T)); faces +X,-X,+Y,-Y,+Z,-Z
+__device__ __forceinline__ int cube_axis(int tab, int f, int k) {
+    constexpr signed char kM[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+    constexpr signed char kS[6][3] = {{0, 0, -1}, {0, 0, 1}, {1, 0, 0}, {1, 0, 0}, {1, 0, 0}, {-1, 0, 0}};
+    constexpr signed char kT[6][3] = {{0, -1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}, {0, -1, 0}, {0, -1, 0}};
+    return tab == 0 ? kM[f][k] : tab == 1 ? kS[f][k] : kT[f][k];
+}
+// texel (i, j) one step off face f -> the adjacent face's texel (exact integer form, see the oracle's cube_adjacent)
+__device__ __forceinline__ void cube_adjacent(int f, int i, int j, int size, int& nf, int& ni, int& nj) {
+    const int a = 2 * i + 1 - size, b = 2 * j + 1 - size;
+    int P[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) P[k] = size * cube_axis(0, f, k) + a * cube_axis(1, f, k) + b * cube_axis(2, f, k);
+    int g = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (P[k] == size + 1 || P[k] == -(size + 1)) g = 2 * k + (P[k] < 0 ? 1 : 0);
+    int c[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int v = P[0] * cube_axis(1 + e, g, 0) + P[1] * cube_axis(1 + e, g, 1) + P[2] * cube_axis(1 + e, g, 2);
+        c[e] = (v == size || v == -size) ? (v > 0 ? size - 1 : 0) : (v + size - 1) / 2;
+    }
+    nf = g;
+    ni = c[0];
+    nj = c[1];
+}
 __device__ f3 sample_sky(const HgKernelParams& kp, f3 dir, int level) {
     if (!(kp.use_cube > 0)) return mk(0, 0, 0);
     float x = dir.x, y = dir.y, z = dir.z;
@@ -986,23 +1016,43 @@ __device__ f3 sample_sky(const HgKernelParams& kp, f3 dir, int level) {
     level = level < 0 ? 0 : (level > kp.cube_mips - 1 ? kp.cube_mips - 1 : level);
     int size = kp.cube_size >> level;
     size = size < 1 ? 1 : size;
-    const float4* tex = kp.cube + kp.cube_mip_offset[level] + size_t(face) * size * size;
+    const float4* mip = kp.cube + kp.cube_mip_offset[level];
     float s = (sc / ma + 1.0f) * 0.5f;
     float t = (tc / ma + 1.0f) * 0.5f;
     float u = s * float(size) - 0.5f, v = t * float(size) - 0.5f;
     float fu = floorf(u), fv = floorf(v);
     float fx = u - fu, fy = v - fv;
-    int x0 = int(fu), y0 = int(fv);
-    int x1 = x0 + 1, y1 = y0 + 1;
-    x0 = min(max(x0, 0), size - 1);
-    x1 = min(max(x1, 0), size - 1);
-    y0 = min(max(y0, 0), size - 1);
-    y1 = min(max(y1, 0), size - 1);
-    const float4 c00 = tex[y0 * size + x0], c10 = tex[y0 * size + x1];
-    const float4 c01 = tex[y1 * size + x0], c11 = tex[y1 * size + x1];
+    const int x0 = int(fu), y0 = int(fv);
+    f3 tex[2][2];  // [row][col]
+    int corner = -1;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = x0 + q, j = y0 + r;
+            const bool in_i = i >= 0 && i < size, in_j = j >= 0 && j < size;
+            tex[r][q] = mk(0, 0, 0);
+            if (!in_i && !in_j) {
+                corner = r * 2 + q;
+                continue;
+            }
+            int f = face, ii = i, jj = j;
+            if (!in_i || !in_j) cube_adjacent(face, i, j, size, f, ii, jj);
+            tex[r][q] = xyz(mip[(size_t(f) * size + jj) * size + ii]);
+        }
+    }
+    if (corner >= 0) {  // the average of the other three: same row, same column, diagonal
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k != corner) continue;
+            const int r = k >> 1, q = k & 1;
+            const f3 sum = (tex[r][1 - q] + tex[1 - r][q]) + tex[1 - r][1 - q];
+            tex[r][q] = mk(sum.x / 3.0f, sum.y / 3.0f, sum.z / 3.0f);
+        }
+    }
     const float gx = 1.0f - fx, gy = 1.0f - fy;
-    f3 top = xyz(c00) * gx + xyz(c10) * fx;
-    f3 bot = xyz(c01) * gx + xyz(c11) * fx;
+    f3 top = tex[0][0] * gx + tex[0][1] * fx;
+    f3 bot = tex[1][0] * gx + tex[1][1] * fx;
     return top * gy + bot * fy;
 }
 

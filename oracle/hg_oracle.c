@@ -204,10 +204,39 @@ float hgo_inverted_blackman_harris(float x) {
 }
 
 /* ------------------------------------------------------------------------------------------------
- * Cubemap: manual bilinear within one mip (the build's definition of TextureCube.SampleLevel with an
- * integral level).  D3D face selection, faces +X,-X,+Y,-Y,+Z,-Z.
+ * Cubemap: TextureCube.SampleLevel (HC:201) with an integral level = bilinear within one mip, SEAMLESS as D3D10+
+ * filters every cube map (and as the reference's asset is imported, seamlessCubemap: 1,
+ * resting_place_4k.exr.meta:32): a footprint texel beyond a face edge is read from the adjacent face; at a cube
+ * corner, where only three texels exist, the fourth is their average.  D3D face selection and (s, t) orientation,
+ * faces +X,-X,+Y,-Y,+Z,-Z; texel centres at (i + 0.5) / size.  The kernel (hg_device.h sample_sky) is the same code.
  * ---------------------------------------------------------------------------------------------- */
-static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+/* Face frames: major axis M, s axis S, t axis T as integer unit vectors (sc = dot(d, S), tc = dot(d, T)). */
+static const int CUBE_M[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+static const int CUBE_S[6][3] = {{0, 0, -1}, {0, 0, 1}, {1, 0, 0}, {1, 0, 0}, {1, 0, 0}, {-1, 0, 0}};
+static const int CUBE_T[6][3] = {{0, -1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}, {0, -1, 0}, {0, -1, 0}};
+
+/* Texel (i, j) of face f with i or j one step outside [0, size): the texel of the adjacent face that the extended
+ * face plane crosses into.  Exact integer form: texel centres at odd coordinates of a cube spanning [-size, size]:
+ * P = size M + (2i + 1 - size) S + (2j + 1 - size) T; the component of magnitude size + 1 names the new face; on it
+ * a coordinate of magnitude size (the old face's plane) is the edge texel, any other c is texel (c + size - 1) / 2
+ * (dividing the direction by (size + 1) / size moves a centre by less than half a texel). */
+static void cube_adjacent(int f, int i, int j, int size, int* nf, int* ni, int* nj) {
+    const int a = 2 * i + 1 - size, b = 2 * j + 1 - size;
+    int P[3];
+    for (int k = 0; k < 3; k++) P[k] = size * CUBE_M[f][k] + a * CUBE_S[f][k] + b * CUBE_T[f][k];
+    int g = 0;
+    for (int k = 0; k < 3; k++)
+        if (P[k] == size + 1 || P[k] == -(size + 1)) g = 2 * k + (P[k] < 0 ? 1 : 0);
+    int c[2];
+    for (int e = 0; e < 2; e++) {
+        const int* ax = e == 0 ? CUBE_S[g] : CUBE_T[g];
+        const int v = P[0] * ax[0] + P[1] * ax[1] + P[2] * ax[2];
+        c[e] = (v == size || v == -size) ? (v > 0 ? size - 1 : 0) : (v + size - 1) / 2;
+    }
+    *nf = g;
+    *ni = c[0];
+    *nj = c[1];
+}
 
 void hgo_cube_sample(const hgo_scene* sc, const float dir[3], int32_t level, float rgb[3]) {
     float x = dir[0], y = dir[1], z = dir[2];
@@ -234,25 +263,48 @@ void hgo_cube_sample(const hgo_scene* sc, const float dir[3], int32_t level, flo
     }
     int size = sc->cube_face_size >> level;
     if (size < 1) size = 1;
-    off += (int64_t)face * size * size * 4;
-    const float* tex = sc->cube_texels + off;
+    const float* mip = sc->cube_texels + off;
     float s = (sc_ / ma + 1.0f) * 0.5f;
     float t = (tc / ma + 1.0f) * 0.5f;
     float u = s * (float)size - 0.5f, v = t * (float)size - 0.5f;
     float fu0 = __builtin_floorf(u), fv0 = __builtin_floorf(v);
     float fx = u - fu0, fy = v - fv0;
-    int x0 = (int)fu0, y0 = (int)fv0, x1 = x0 + 1, y1 = y0 + 1;
-    x0 = clampi(x0, 0, size - 1);
-    x1 = clampi(x1, 0, size - 1);
-    y0 = clampi(y0, 0, size - 1);
-    y1 = clampi(y1, 0, size - 1);
+    const int xs[2] = {(int)fu0, (int)fu0 + 1}, ys[2] = {(int)fv0, (int)fv0 + 1};
+    float tex[2][2][3]; /* [row][col][rgb] */
+    int corner = -1;    /* footprint texel with both coordinates off the face */
+    for (int r = 0; r < 2; r++) {
+        for (int q = 0; q < 2; q++) {
+            const int i = xs[q], j = ys[r];
+            const int in_i = i >= 0 && i < size, in_j = j >= 0 && j < size;
+            if (!in_i && !in_j) {
+                corner = r * 2 + q;
+                continue;
+            }
+            int f = face, ii = i, jj = j;
+            if (!in_i || !in_j) cube_adjacent(face, i, j, size, &f, &ii, &jj);
+            const float* p = mip + (((int64_t)f * size + jj) * size + ii) * 4;
+            for (int c = 0; c < 3; c++) tex[r][q][c] = p[c];
+        }
+    }
+    if (corner >= 0) { /* the average of the other three: same row, same column, diagonal */
+        const int r = corner >> 1, q = corner & 1;
+        for (int c = 0; c < 3; c++)
+            tex[r][q][c] = ((tex[r][1 - q][c] + tex[1 - r][q][c]) + tex[1 - r][1 - q][c]) / 3.0f;
+    }
     for (int c = 0; c < 3; c++) {
-        float c00 = tex[((int64_t)y0 * size + x0) * 4 + c], c10 = tex[((int64_t)y0 * size + x1) * 4 + c];
-        float c01 = tex[((int64_t)y1 * size + x0) * 4 + c], c11 = tex[((int64_t)y1 * size + x1) * 4 + c];
-        float top = c00 * (1.0f - fx) + c10 * fx;
-        float bot = c01 * (1.0f - fx) + c11 * fx;
+        float top = tex[0][0][c] * (1.0f - fx) + tex[0][1][c] * fx;
+        float bot = tex[1][0][c] * (1.0f - fx) + tex[1][1][c] * fx;
         rgb[c] = top * (1.0f - fy) + bot * fy;
     }
+}
+
+/* Exposed for the adjacency unit test (tests/test_cubemap.py). */
+void hgo_cube_adjacent(int32_t f, int32_t i, int32_t j, int32_t size, int32_t out[3]) {
+    int nf, ni, nj;
+    cube_adjacent(f, i, j, size, &nf, &ni, &nj);
+    out[0] = nf;
+    out[1] = ni;
+    out[2] = nj;
 }
 
 /* sample_sky, :196-204.  level is already the int the reference passes. */

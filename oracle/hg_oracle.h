@@ -72,6 +72,8 @@ float hgo_triangle_t(const float o[3], const float d[3], const float v0[3], cons
                      float* u, float* v, float* orientation);
 float hgo_aabb_t(const float a[3], const float b[3], const float o[3], const float inv_d[3]);
 void hgo_cube_sample(const hgo_scene* scene, const float dir[3], int32_t level, float rgb[3]);
+/* Seamless cube filtering: the adjacent face's texel for texel (i, j) one step outside face f (out: face, i, j). */
+void hgo_cube_adjacent(int32_t f, int32_t i, int32_t j, int32_t size, int32_t out[3]);
 void hgo_fmath(int32_t fn, const float* x, float* y, int64_t n);
 
 #ifdef __cplusplus

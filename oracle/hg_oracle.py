@@ -75,6 +75,8 @@ def lib():
         L.hgo_stack_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_int32), C.c_int32]
         L.hgo_cube_sample.restype = None
         L.hgo_cube_sample.argtypes = [C.POINTER(HgoScene), fp, C.c_int32, fp]
+        L.hgo_cube_adjacent.restype = None
+        L.hgo_cube_adjacent.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -133,3 +135,20 @@ def stack_stats(reset: bool = False) -> tuple[int, int]:
     n, d = C.c_uint64(0), C.c_int32(0)
     lib().hgo_stack_stats(C.byref(n), C.byref(d), 1 if reset else 0)
     return int(n.value), int(d.value)
+
+
+def cube_adjacent(face: int, i: int, j: int, size: int) -> tuple[int, int, int]:
+    out = (C.c_int32 * 3)()
+    lib().hgo_cube_adjacent(face, i, j, size, out)
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def cube_sample(cubemap, d, level: int) -> np.ndarray:
+    s = HgoScene()
+    tex = np.ascontiguousarray(cubemap.texels, dtype=np.float32)
+    s.cube_texels = tex.ctypes.data
+    s.cube_face_size, s.cube_mips = cubemap.face_size, cubemap.n_mips
+    dv = (C.c_float * 3)(*[float(x) for x in d])
+    rgb = (C.c_float * 3)()
+    lib().hgo_cube_sample(C.byref(s), dv, level, rgb)
+    return np.array(list(rgb), dtype=np.float32)
