@@ -1,0 +1,69 @@
+"""Sanitizer builds of the native host code (SURVEY.md §5 "race detection / sanitizers"; GPU sanitizers are not
+available on this pool, so the HIP kernels are covered by the bit-exact parity tests instead):
+
+- the CPU oracle under AddressSanitizer + UndefinedBehaviorSanitizer (oracle/sanitize_main.c, make -C oracle
+  sanitize), rendering golden cases on several pthreads: no report, and the image bit-identical to the regular
+  oracle build's;
+- the oracle's BVH builder (BVHGenerator.cs restated) under the same sanitizers;
+- the product's parallel BLAS builder hg_build_blas_mt (std::thread pool, atomics; csrc/hg_host.cpp) under
+  ThreadSanitizer (halogen-pathtracer_amd/host/tsan_blas.cpp, make -C halogen-pathtracer_amd tsan), large enough to
+  take the rank-parallel partition, with 2, 5 and 16 workers: no data race, output equal to the sequential build."""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import cases
+import hg_oracle
+from halogen import host_files
+
+ROOT = Path(__file__).resolve().parents[1]
+ASAN = ROOT / "oracle" / "build" / "hg_oracle_asan"
+TSAN = ROOT / "halogen-pathtracer_amd" / "build" / "tsan_blas"
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+
+
+@pytest.fixture(scope="module")
+def asan():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "sanitize"], check=True)
+    return ASAN
+
+
+@pytest.fixture(scope="module")
+def tsan():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "halogen-pathtracer_amd"), "tsan"], check=True)
+    return TSAN
+
+
+def run(cmd):
+    r = subprocess.run([str(c) for c in cmd], env=ENV, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", ["c1_64", "glass_64x36", "dragon1_64x36", "c1_32_tritests"])
+def test_oracle_under_asan_ubsan(built, asan, tmp_path, name):
+    packed, params, cube, frames, acc = cases.setup(name)
+    host_files.write_scene(packed, tmp_path / "s.hgscene")
+    (tmp_path / "p.bin").write_bytes(bytes(params))
+    cmd = [asan, "render", tmp_path / "s.hgscene", tmp_path / "p.bin", frames, 3, tmp_path / "out.f32"]
+    if cube is not None:
+        host_files.write_cubemap(cube, tmp_path / "c.hgcube")
+        cmd.append(tmp_path / "c.hgcube")
+    run(cmd)
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    got = np.fromfile(tmp_path / "out.f32", dtype=np.float32).reshape(H, W, 4)
+    want, _ = hg_oracle.render(packed, params, frames, True, cubemap=cube)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_oracle_bvh_builder_under_asan_ubsan(asan):
+    assert "BVH entries" in run([asan, "blas", 20000, 3])
+
+
+def test_parallel_blas_builder_under_tsan(tsan):
+    out = run([tsan, 40000, 7, 2, 5, 16])
+    assert out.count("identical") == 3
