@@ -45,7 +45,6 @@ struct hg_ctx {
     DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
     DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     DevBuf pool;                 // path-pool kernel: per-wave path slots
-    DevBuf cam_a, cam_b;         // camera-ray pass: primary rays of this launch chunk
     DevBuf tile_cost, tile_order;  // cost-ordered dispatch: per local tile, wave-clock cost / dispatch order
     bool tile_cost_valid = false;  // tile_cost holds the previous regen/stream launch's costs for this tiling
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early

@@ -99,9 +99,6 @@
 #ifndef HG_REGEN_PRIO
 #define HG_REGEN_PRIO 1  // regenerating kernel: wave priority raised during get_ray_intersection (C2 +1 %, C5 +2 %,
 #endif                   // tools/sweeps/sweep69.txt)
-#ifndef HG_CAMERA_PASS
-#define HG_CAMERA_PASS 0  // streaming kernel, spp 1: primary rays precomputed by a coherent pass (hg_camera_rays)
-#endif
 #ifndef HG_STACK_TOP
 #define HG_STACK_TOP 0  // streaming traversal: keep the stack's top entry in a register (pops off the LDS latency)
 #endif
@@ -116,6 +113,9 @@
 #endif
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
+#endif
+#ifndef HG_LDS_ACC
+#define HG_LDS_ACC 1  // streaming kernel, spp 1 and unsplit: the lane's accumulator lives in LDS for the launch
 #endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
@@ -158,10 +158,6 @@ struct HgKernelParams {
     // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
     int32_t frame_split;
     float4* __restrict__ frame_color;
-    // camera-ray pass (spp == 1): the primary ray of every (launch frame f, slot) precomputed by hg_camera_rays,
-    // (o.xyz, d.x) in cam_a and (d.y, d.z) in cam_b at [f * n_local_tiles * 64 + slot]; null: rays made inline
-    float4* __restrict__ cam_a;
-    float2* __restrict__ cam_b;
     float4* __restrict__ pool;  // path-pool kernel: per-wave path slots (hg_pool.hip)
     // cost-ordered dispatch (regen / stream kernels): wave w traces local tile tile_order[w % n_local_tiles] (null:
     // tile w % n_local_tiles) and adds its wave-clock cost to tile_cost[tile] (null: not recorded).  Any permutation

@@ -99,6 +99,26 @@ struct LaneVec {
     }
 };
 constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
+// Streaming kernel: one more word per lane.  With spp == 1 and an unsplit launch the sample sum is never needed
+// (the frame's colour is the path's colour), and its 3 words plus the extra one hold the lane's accumulator value
+// for the whole launch (HG_LDS_ACC): the per-frame blend acc*(1-w) + c*w reads and writes LDS instead of a global
+// read-modify-write per pixel-frame; the value comes from global memory once at the wave's start and goes back once
+// at its end.  Same operations in the same order: bit-identical.
+constexpr uint32_t kStreamLdsState = 10;
+struct LaneAcc {
+    uint32_t idx, stride;  // word idx + k*stride, k = 0..3
+    __device__ __forceinline__ float4 get() const {
+        return make_float4(__uint_as_float(hg_lds_stack[idx]), __uint_as_float(hg_lds_stack[idx + stride]),
+                           __uint_as_float(hg_lds_stack[idx + 2 * stride]),
+                           __uint_as_float(hg_lds_stack[idx + 3 * stride]));
+    }
+    __device__ __forceinline__ void set(float4 v) const {
+        hg_lds_stack[idx] = __float_as_uint(v.x);
+        hg_lds_stack[idx + stride] = __float_as_uint(v.y);
+        hg_lds_stack[idx + 2 * stride] = __float_as_uint(v.z);
+        hg_lds_stack[idx + 3 * stride] = __float_as_uint(v.w);
+    }
+};
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
 // written by hg_order_tiles before this launch and never during it).
@@ -425,39 +445,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
-// Camera-ray pass: the primary ray of every (frame, pixel slot) of a launch, thread per ray, so the megakernel's
-// path regeneration loads 24 B instead of running get_ray (:996-1013) under divergence.  Same function, same
-// inputs (FrameCount, pixel hash, SobolDimensionOffset 0: with spp == 1 every path starts a frame), same bits.
-__global__ __launch_bounds__(256) void hg_camera_rays(const HgKernelParams kp) {
-    const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= uint64_t(n_slots) * uint32_t(kp.n_frames)) return;
-    const uint32_t f = uint32_t(i / n_slots), slot = uint32_t(i % n_slots);
-    const int gtile = kp.rank + int(slot >> 6) * kp.n_ranks;
-    const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (slot & 7u);
-    const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + ((slot >> 3) & 7u);
-    if (px >= kp.Wu || py >= kp.Hu) return;
-    const Sampler smp{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
-    const Ray r = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);
-    kp.cam_a[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    kp.cam_b[i] = make_float2(r.d.y, r.d.z);
-}
-
-hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream) {
-    const uint64_t n = uint64_t(kp.n_local_tiles) * 64u * uint32_t(kp.n_frames);
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(hg_camera_rays, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, stream, kp);
-    return hipGetLastError();
-}
-
-__device__ __forceinline__ Ray load_camera_ray(const HgKernelParams& kp, uint32_t f, uint32_t slot) {
-    const size_t i = size_t(f) * (size_t(uint32_t(kp.n_local_tiles)) * 64u) + slot;
-    const float4 a = kp.cam_a[i];
-    const float2 b = kp.cam_b[i];
-    return Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)};
-}
-
-template <bool kCounters, bool kCamPass>
+template <bool kCounters, bool kLdsAcc>
 __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
@@ -473,8 +461,10 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
     const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
     const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
-    const LeafShare ls{(lds_depth + kRegenLdsState) * blockDim.x + (threadIdx.x >> 6) * (kLeafShareWords * 64u)};
+    const LaneAcc s_acc{sb + 6 * blockDim.x, blockDim.x};  // the sum's words (+1): used only when lds_acc
+    const LeafShare ls{(lds_depth + kStreamLdsState) * blockDim.x + (threadIdx.x >> 6) * (kLeafShareWords * 64u)};
     const uint32_t nm = uint32_t(kp.n_meshes);
+    constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
     bool work;
     uint32_t px, py;
     {
@@ -494,12 +484,12 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     Trav tv;
     tv.mi = nm;
     if (work) {
-        ray = kCamPass ? load_camera_ray(kp, f_begin, uint32_t(local_tile) * 64u + lane)
-                       : camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
+        ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
         s_thr.set(mk(1, 1, 1));
         s_col.set(mk(0, 0, 0));
-        s_sum.set(mk(0, 0, 0));
+        if (lds_acc) s_acc.set(kp.acc[size_t(uint32_t(local_tile)) * 64u + lane]);
+        else s_sum.set(mk(0, 0, 0));
         trav_begin(kp, ray, tv, c);
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
@@ -570,7 +560,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             if (kCounters) tp = phase_mark(kp, 12, tp);
 #endif
             if (!alive) {
-                f3 sum = s_sum.get() + col;  // RayColor += trace_ray(...)
+                // RayColor += trace_ray(...); with lds_acc (spp 1) the sum is the path's colour (0 + col == col)
+                f3 sum = lds_acc ? col : s_sum.get() + col;
                 ++fs;
                 bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
@@ -581,8 +572,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                         kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
-                        float4* slot = kp.acc + slot_i;
-                        float4 acc = *slot;
+                        float4 acc = lds_acc ? s_acc.get() : kp.acc[slot_i];
                         if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
                             const float w = rcp_exact(float(smp.frame));
                             const float k = 1.0f - w;
@@ -591,7 +581,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                         } else {
                             acc = make_float4(color.x, color.y, color.z, 1.0f);
                         }
-                        *slot = acc;
+                        if (lds_acc) s_acc.set(acc);
+                        else kp.acc[slot_i] = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
                     if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
@@ -602,11 +593,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                         ms = MediumStack{0ull, 0};
                     }
                 }
-                s_sum.set(sum);
+                if (!lds_acc) s_sum.set(sum);
                 if (next) {
-                    if (kCamPass) {  // spp == 1: `next` is always a new frame, fs >> 16
-                        ray = load_camera_ray(kp, fs >> 16, uint32_t(local_tile) * 64u + lane);
-                    } else {
+                    {
                         const int gtile = kp.rank + local_tile * kp.n_ranks;
                         const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
                         const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
@@ -639,6 +628,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 #endif
         if (kCounters) cyc_shade += wave_clock();
     }
+    if (lds_acc && fs >= 0x10000u)  // unsplit: a lane that traced its pixel ended on frame f_end > f_begin = 0
+        kp.acc[size_t(uint32_t(local_tile)) * 64u + lane] = s_acc.get();
     record_tile_cost(lane);
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
@@ -663,14 +654,14 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool count
     const int tiles_per_block = block / 64;
     const int64_t grid = (int64_t(kp.n_local_tiles) * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
     if (grid == 0) return hipSuccess;
-    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4 +
+    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kStreamLdsState) * size_t(block) * 4 +
                        (HG_LEAF_DIST ? size_t(kLeafShareWords) * size_t(block) * 4 : 0);
-    const bool cam = kp.cam_a != nullptr;
-    if (counters && cam)
+    const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
+    if (counters && lds_acc)
         hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else if (counters)
         hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
-    else if (cam)
+    else if (lds_acc)
         hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else
         hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);

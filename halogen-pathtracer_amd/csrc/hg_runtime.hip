@@ -25,7 +25,6 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
 hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, hipStream_t stream);
-hipError_t hg_launch_camera_rays(const HgKernelParams& kp, hipStream_t stream);
 #ifndef HG_WITH_VARIANTS
 #define HG_WITH_VARIANTS 0  // A/B variants (wavefront pipeline, path pool): make VARIANTS=1
 #endif
@@ -367,7 +366,7 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool, &c->cam_a, &c->cam_b,
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool,
                       &c->tile_cost, &c->tile_order})
         release(*b);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
@@ -767,22 +766,6 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 return rc;
             }
         }
-        // camera-ray pass (streaming kernel, spp 1: every path starts a frame, so its primary ray depends on the
-        // pixel and FrameCount only): 24 B per (frame, slot) of a chunk, under the same cap
-        const bool cam_pass = HG_CAMERA_PASS && stream_k && kp.spp == 1 && tiles > 0;
-        if (cam_pass) {
-            const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
-            chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
-            const size_t n = size_t(tiles) * 64 * size_t(std::min(n_frames, chunk_max));
-            if (int rc = ensure(c, c->cam_a, n * sizeof(float4))) {
-                c->free_events.push_back(ev);
-                return rc;
-            }
-            if (int rc = ensure(c, c->cam_b, n * sizeof(float2))) {
-                c->free_events.push_back(ev);
-                return rc;
-            }
-        }
         const int mgrid = int((units * split + mblock / 64 - 1) / (mblock / 64));
         if (pool_k) {
             if (int rc = ensure(c, c->pool, size_t(mgrid) * hg_pool_slots() * 8 * sizeof(float4))) {
@@ -805,8 +788,6 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
             HgKernelParams kc = kp;
             kc.frame_color = static_cast<float4*>(c->frame_color.p);
-            kc.cam_a = cam_pass ? static_cast<float4*>(c->cam_a.p) : nullptr;
-            kc.cam_b = cam_pass ? static_cast<float2*>(c->cam_b.p) : nullptr;
             // cost-ordered dispatch: the previous launch's per-tile wave times order this launch's tiles, most
             // expensive first, so the launch's drain tail holds the cheap tiles (any order gives the same image)
             kc.tile_cost = nullptr;
@@ -837,7 +818,6 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     }
                     c->tile_cost_valid = e == hipSuccess;
                 }
-                if (e == hipSuccess && cam_pass) e = hg_launch_camera_rays(kc, c->stream);
                 if (e == hipSuccess)
                     e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
                     : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
