@@ -370,6 +370,68 @@ struct Stack {
 };
 using MegaStack = Stack<HG_MEGA_LDS_STACK>;
 
+// Row-major per-lane LDS layout of a one-wave workgroup (the streaming kernel): word (row, lane) = row * 64 + lane.
+// Every access is the lane's one base address plus a compile-time row offset (a ds_read / ds_write immediate), so no
+// per-variable LDS addresses occupy registers.
+template <uint32_t kRow>
+struct RowVec3 {  // a float3 in rows kRow .. kRow+2
+    uint32_t lane;
+    __device__ __forceinline__ f3 get() const {
+        return mk(__uint_as_float(hg_lds_stack[kRow * 64u + lane]), __uint_as_float(hg_lds_stack[(kRow + 1) * 64u + lane]),
+                  __uint_as_float(hg_lds_stack[(kRow + 2) * 64u + lane]));
+    }
+    __device__ __forceinline__ void set(f3 v) const {
+        hg_lds_stack[kRow * 64u + lane] = __float_as_uint(v.x);
+        hg_lds_stack[(kRow + 1) * 64u + lane] = __float_as_uint(v.y);
+        hg_lds_stack[(kRow + 2) * 64u + lane] = __float_as_uint(v.z);
+    }
+};
+template <uint32_t kRow>
+struct RowVec4 {  // a float4 in rows kRow .. kRow+3
+    uint32_t lane;
+    __device__ __forceinline__ float4 get() const {
+        return make_float4(__uint_as_float(hg_lds_stack[kRow * 64u + lane]),
+                           __uint_as_float(hg_lds_stack[(kRow + 1) * 64u + lane]),
+                           __uint_as_float(hg_lds_stack[(kRow + 2) * 64u + lane]),
+                           __uint_as_float(hg_lds_stack[(kRow + 3) * 64u + lane]));
+    }
+    __device__ __forceinline__ void set(float4 v) const {
+        hg_lds_stack[kRow * 64u + lane] = __float_as_uint(v.x);
+        hg_lds_stack[(kRow + 1) * 64u + lane] = __float_as_uint(v.y);
+        hg_lds_stack[(kRow + 2) * 64u + lane] = __float_as_uint(v.z);
+        hg_lds_stack[(kRow + 3) * 64u + lane] = __float_as_uint(v.w);
+    }
+};
+// The traversal stack in rows kRow .. kRow+kLds-1 (entry k of the lane at row kRow + k), deeper entries in the lane's
+// global spill column, as Stack.
+template <uint32_t kLds, uint32_t kRow>
+struct RowStack {
+    uint32_t lane;
+    uint32_t* spill;
+    uint32_t spill_stride;
+    __device__ __forceinline__ void store(uint32_t slot, uint32_t v) const {
+        if (__builtin_expect(slot < kLds, 1)) hg_lds_stack[(kRow + slot) * 64u + lane] = v;
+        else spill[(slot - kLds) * spill_stride] = v;
+    }
+    __device__ __forceinline__ uint32_t load(uint32_t slot) const {
+        if (__builtin_expect(slot < kLds, 1)) return hg_lds_stack[(kRow + slot) * 64u + lane];
+        uint32_t v = spill[(slot - kLds) * spill_stride];
+        asm volatile("" : "+v"(v));
+        return v;
+    }
+    __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const { store(sp++, v); }
+    __device__ __forceinline__ uint32_t pop(uint32_t& sp) const { return load(--sp); }
+    __device__ __forceinline__ void push_c(uint32_t& sp, uint32_t& top, uint32_t v) const {
+        store(sp++, top);
+        top = v;
+    }
+    __device__ __forceinline__ uint32_t pop_c(uint32_t& sp, uint32_t& top) const {
+        const uint32_t v = top;
+        top = load(--sp);
+        return v;
+    }
+};
+
 // first mesh index >= m whose cull bit is set (meshes >= 64 carry no bit and are always live); n if none
 __device__ __forceinline__ uint32_t next_live_mesh(uint64_t live, uint32_t m, uint32_t n) {
     uint32_t r = 64u;

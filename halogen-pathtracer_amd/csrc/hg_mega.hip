@@ -105,6 +105,9 @@ constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
 // read-modify-write per pixel-frame; the value comes from global memory once at the wave's start and goes back once
 // at its end.  Same operations in the same order: bit-identical.
 constexpr uint32_t kStreamLdsState = 10;
+// Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
+// 6-8 or the accumulator 6-9 (lds_acc), the distributed leaf test 10-12, the traversal stack from row 13.
+constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState, kRowStack = kRowLeaf + 3;
 struct LaneAcc {
     uint32_t idx, stride;  // word idx + k*stride, k = 0..3
     __device__ __forceinline__ float4 get() const {
@@ -449,7 +452,8 @@ template <bool kCounters, bool kLdsAcc>
 __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
-    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // one wave per workgroup (launched with 64 threads): wave = workgroup
+    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
     int local_tile;
     uint32_t chunk;
@@ -457,12 +461,12 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
-    const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
-    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
-    const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
-    const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
-    const LaneAcc s_acc{sb + 6 * blockDim.x, blockDim.x};  // the sum's words (+1): used only when lds_acc
-    const LeafShare ls{(lds_depth + kStreamLdsState) * blockDim.x + (threadIdx.x >> 6) * (kLeafShareWords * 64u)};
+    const RowStack<HG_MEGA_LDS_STACK, kRowStack> stk{lane, kp.spill + blockIdx.x * 64u + lane, kp.spill_stride};
+    const RowVec3<kRowThr> s_thr{lane};
+    const RowVec3<kRowCol> s_col{lane};
+    const RowVec3<kRowSum> s_sum{lane};
+    const RowVec4<kRowSum> s_acc{lane};  // the sum's words (+1): used only when lds_acc
+    const LeafShare ls{kRowLeaf * 64u};
     const uint32_t nm = uint32_t(kp.n_meshes);
     constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
     bool work;
@@ -651,11 +655,12 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 }
 
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
-    const int tiles_per_block = block / 64;
-    const int64_t grid = (int64_t(kp.n_local_tiles) * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
+    (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
+    const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
     if (grid == 0) return hipSuccess;
-    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kStreamLdsState) * size_t(block) * 4 +
-                       (HG_LEAF_DIST ? size_t(kLeafShareWords) * size_t(block) * 4 : 0);
+    block = 64;
+    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t);
     const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
     if (counters && lds_acc)
         hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
