@@ -84,21 +84,9 @@ size_t hg_mega_lds_bytes(uint32_t stack_depth, int block) {
 // the traversal's register budget: bounceTypes[3] + the bounce index in one word (host guarantees maxBounces <=
 // HG_REGEN_MAX_BOUNCES), frame + sample index in another (n_frames, spp < 2^16, host-chunked), the pixel's ndc /
 // accumulator slot recomputed at each regeneration.
-// A float3 of per-lane path state parked in LDS ([component][lane] after the traversal stack): the throughput,
-// radiance and sample sum are touched once per bounce, so they stay out of the registers the traversal needs.
-struct LaneVec {
-    uint32_t idx, stride;
-    __device__ __forceinline__ f3 get() const {
-        return mk(__uint_as_float(hg_lds_stack[idx]), __uint_as_float(hg_lds_stack[idx + stride]),
-                  __uint_as_float(hg_lds_stack[idx + 2 * stride]));
-    }
-    __device__ __forceinline__ void set(f3 v) const {
-        hg_lds_stack[idx] = __float_as_uint(v.x);
-        hg_lds_stack[idx + stride] = __float_as_uint(v.y);
-        hg_lds_stack[idx + 2 * stride] = __float_as_uint(v.z);
-    }
-};
-constexpr uint32_t kRegenLdsState = 9;  // LaneVec words per lane
+// Per-lane path state parked in LDS (RowVec3 / RowVec4 rows, hg_device.h): the throughput, radiance and sample sum
+// are touched once per bounce, so they stay out of the registers the traversal needs.
+constexpr uint32_t kRegenLdsState = 9;  // words per lane: throughput, radiance, sample sum
 // Streaming kernel: one more word per lane.  With spp == 1 and an unsplit launch the sample sum is never needed
 // (the frame's colour is the path's colour), and its 3 words plus the extra one hold the lane's accumulator value
 // for the whole launch (HG_LDS_ACC): the per-frame blend acc*(1-w) + c*w reads and writes LDS instead of a global
@@ -108,20 +96,7 @@ constexpr uint32_t kStreamLdsState = 10;
 // Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
 // 6-8 or the accumulator 6-9 (lds_acc), the distributed leaf test 10-12, the traversal stack from row 13.
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState, kRowStack = kRowLeaf + 3;
-struct LaneAcc {
-    uint32_t idx, stride;  // word idx + k*stride, k = 0..3
-    __device__ __forceinline__ float4 get() const {
-        return make_float4(__uint_as_float(hg_lds_stack[idx]), __uint_as_float(hg_lds_stack[idx + stride]),
-                           __uint_as_float(hg_lds_stack[idx + 2 * stride]),
-                           __uint_as_float(hg_lds_stack[idx + 3 * stride]));
-    }
-    __device__ __forceinline__ void set(float4 v) const {
-        hg_lds_stack[idx] = __float_as_uint(v.x);
-        hg_lds_stack[idx + stride] = __float_as_uint(v.y);
-        hg_lds_stack[idx + 2 * stride] = __float_as_uint(v.z);
-        hg_lds_stack[idx + 3 * stride] = __float_as_uint(v.w);
-    }
-};
+constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
 // written by hg_order_tiles before this launch and never during it).
@@ -249,7 +224,8 @@ template <bool kCounters>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
-    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // one wave per workgroup (launched with 64 threads): wave = workgroup; LDS rows as the streaming kernel's
+    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
     int local_tile;
     uint32_t chunk;
@@ -257,10 +233,10 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
-    const MegaStack stk{threadIdx.x, blockDim.x, kp.spill + blockIdx.x * blockDim.x + threadIdx.x, kp.spill_stride};
-    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
-    const uint32_t sb = lds_depth * blockDim.x + threadIdx.x;
-    const LaneVec s_thr{sb, blockDim.x}, s_col{sb + 3 * blockDim.x, blockDim.x}, s_sum{sb + 6 * blockDim.x, blockDim.x};
+    const RowStack<HG_MEGA_LDS_STACK, kRegenRowStack> stk{lane, kp.spill + blockIdx.x * 64u + lane, kp.spill_stride};
+    const RowVec3<kRowThr> s_thr{lane};
+    const RowVec3<kRowCol> s_col{lane};
+    const RowVec3<kRowSum> s_sum{lane};
     bool work;
     uint32_t px, py;
     {
@@ -433,10 +409,12 @@ hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) 
 }
 
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
-    const int tiles_per_block = block / 64;
-    const int64_t grid = (int64_t(kp.n_local_tiles) * kp.frame_split + tiles_per_block - 1) / tiles_per_block;
+    (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
+    block = 64;
+    const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
     if (grid == 0) return hipSuccess;
-    const size_t lds = hg_mega_lds_bytes(kp.stack_depth, block) + size_t(kRegenLdsState) * size_t(block) * 4;
+    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const size_t lds = size_t(kRegenRowStack + lds_depth) * 64u * sizeof(uint32_t);
     if (counters)
         hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
     else

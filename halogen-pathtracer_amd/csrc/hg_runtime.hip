@@ -729,9 +729,8 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweeps/sweep12.txt), 256 for the lockstep one
         const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
-        const bool stream_k0 = regen && kern == HG_KERNEL_MEGA_STREAM;
-        // the streaming kernel runs one wave per workgroup (its LDS row layout assumes it)
-        const int mblock = (pool_k || stream_k0) ? 64 : (c->block == 128 ? (regen ? 64 : 256) : c->block);
+        // the regenerating / streaming kernels run one wave per workgroup (their LDS row layout assumes it)
+        const int mblock = regen ? 64 : (c->block == 128 ? 256 : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
         // about 6x (formerly 16x, 12x) as many waves as the GPU holds at once (short waves: small drain tail; a rank's 1/N share
         // of the tiles at N GPUs still fills the GPU); the per-frame colours are then blended in frame order
