@@ -25,6 +25,7 @@ struct hg_ctx {
     DevBuf spheres, meshes, materials, nodes, leaves, tri_a, tri_b, tri_c, normals;
     int32_t n_spheres = 0, n_meshes = 0, n_materials = 0, n_tris = 0, n_nodes = 0;
     uint32_t stack_depth = 2;
+    uint32_t hot_records = 0;  // HG_NODE_CACHE: device records [0, hot_records) are the BLAS tops (hot_prefix)
 
     // cubemap
     DevBuf cube;

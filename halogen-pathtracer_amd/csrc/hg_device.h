@@ -904,9 +904,27 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(act)))) break;
         c.node_rounds += wave_once();
         if (act && !(t.node & HG_LEAF_BIT)) {
+#if HG_NODE_CACHE
+            // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
+            float4 a_lo, a_hi, b_lo, b_hi;
+            if (t.node < kp.hot_records) {
+                const float4* cr = reinterpret_cast<const float4*>(hg_lds_stack + HG_STREAM_CACHE_ROW * 64u) + 4u * t.node;
+                a_lo = cr[0];
+                a_hi = cr[1];
+                b_lo = cr[2];
+                b_hi = cr[3];
+            } else {
+                const uint32_t ro = t.node << 6;
+                a_lo = ld_off(kp.nodes, ro);
+                a_hi = ld_off(kp.nodes, ro + 16);
+                b_lo = ld_off(kp.nodes, ro + 32);
+                b_hi = ld_off(kp.nodes, ro + 48);
+            }
+#else
             const uint32_t ro = t.node << 6;
             const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
                          b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
+#endif
             const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
 #if HG_NODE_PREFETCH
             // after all four loads have landed (vmcnt retires in order: a wait for a later load would include it)

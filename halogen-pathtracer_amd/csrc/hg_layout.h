@@ -117,11 +117,18 @@
 #ifndef HG_LDS_ACC
 #define HG_LDS_ACC 1  // streaming kernel, spp 1 and unsplit: the lane's accumulator lives in LDS for the launch
 #endif
+#ifndef HG_NODE_CACHE
+#define HG_NODE_CACHE 0  // streaming kernel: the top records of every BLAS (BFS) copied into LDS per wave (records,
+#endif                   // a multiple of 4: 4 records = one 64-lane LDS row)
+#define HG_STREAM_CACHE_ROW 13  // its first LDS row (after the per-lane state rows, hg_mega.hip kRowStack)
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif
 #ifndef HG_MEGA_LDS_STACK
 #define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
+#endif
+#ifndef HG_STREAM_LDS_STACK
+#define HG_STREAM_LDS_STACK HG_MEGA_LDS_STACK  // the same for the streaming kernel
 #endif
 
 struct alignas(16) HgDevMesh {
@@ -167,6 +174,7 @@ struct HgKernelParams {
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
+    uint32_t hot_records;  // HG_NODE_CACHE: node records [0, hot_records) are served from the wave's LDS copy
     uint32_t descent_t;    // relaxed while-while threshold (hg_device.h isect_meshes), 0 = classic while-while
     uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
     uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)

@@ -95,7 +95,9 @@ constexpr uint32_t kRegenLdsState = 9;  // words per lane: throughput, radiance,
 constexpr uint32_t kStreamLdsState = 10;
 // Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
 // 6-8 or the accumulator 6-9 (lds_acc), the distributed leaf test 10-12, the traversal stack from row 13.
-constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState, kRowStack = kRowLeaf + 3;
+constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
+constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
+static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
 constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     tile_cost_begin(kp, lane, local_tile, chunk < split);
     const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
     const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
-    const RowStack<HG_MEGA_LDS_STACK, kRowStack> stk{lane, kp.spill + blockIdx.x * 64u + lane, kp.spill_stride};
+    const RowStack<HG_STREAM_LDS_STACK, kRowStack> stk{lane, kp.spill + blockIdx.x * 64u + lane, kp.spill_stride};
     const RowVec3<kRowThr> s_thr{lane};
     const RowVec3<kRowCol> s_col{lane};
     const RowVec3<kRowSum> s_sum{lane};
@@ -447,6 +449,14 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     const LeafShare ls{kRowLeaf * 64u};
     const uint32_t nm = uint32_t(kp.n_meshes);
     constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
+#if HG_NODE_CACHE
+    {  // the wave's copy of the hot node records (written before any lane reads it: one wave per workgroup)
+        float4* cache = reinterpret_cast<float4*>(hg_lds_stack + kRowCache * 64u);
+        const uint32_t nf4 = 4u * (kp.hot_records < HG_NODE_CACHE ? kp.hot_records : uint32_t(HG_NODE_CACHE));
+        for (uint32_t i = lane; i < nf4; i += 64u) cache[i] = kp.nodes[i];
+        wave_lds_sync();
+    }
+#endif
     bool work;
     uint32_t px, py;
     {
@@ -637,7 +647,7 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool count
     const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
     if (grid == 0) return hipSuccess;
     block = 64;
-    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const uint32_t lds_depth = kp.stack_depth < HG_STREAM_LDS_STACK ? kp.stack_depth : HG_STREAM_LDS_STACK;
     const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t);
     const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
     if (counters && lds_acc)

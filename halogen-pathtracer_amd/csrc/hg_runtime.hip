@@ -174,6 +174,58 @@ bool mesh_cull_boxes(const hg_mat4& w2l, const BVHEntry& A, const BVHEntry& B, H
     return world_box(l2w, A, dm.cull_a_lo, dm.cull_a_hi) && world_box(l2w, B, dm.cull_b_lo, dm.cull_b_hi);
 }
 
+// Hot-node prefix (HG_NODE_CACHE > 0): renumber the device records so that the first `k` are the top of every
+// mesh's BLAS in breadth-first order (all meshes' roots, then their inner children, level by level; a node's two
+// child records stay adjacent), the records every traversal starts with.  The streaming kernel copies records
+// [0, hot) into LDS per wave and serves node fetches below `hot` from there.  Traversal follows refs, so the
+// numbering changes no visit order or result.  Returns the number of hot records.
+uint32_t ubits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32_t k) {
+    const uint32_t n = uint32_t(rec.size() / 4);
+    k = std::min(k, n);
+    if (k == 0) return 0;
+    std::vector<uint32_t> newi(n, HG_NONE);
+    std::vector<uint32_t> queue;
+    uint32_t next = 0;
+    for (const HgDevMesh& m : dm)
+        if (!(m.root_ref & HG_LEAF_BIT) && m.root_ref < n && newi[m.root_ref] == HG_NONE && next < k) {
+            newi[m.root_ref] = next++;
+            queue.push_back(m.root_ref);
+        }
+    for (size_t q = 0; q < queue.size() && next < k; ++q) {
+        const uint32_t r = queue[q];
+        for (int child = 0; child < 2 && next < k; ++child) {
+            const uint32_t ref = ubits(child == 0 ? rec[4 * size_t(r)].w : rec[4 * size_t(r) + 1].w);
+            if ((ref & HG_LEAF_BIT) || ref >= n || newi[ref] != HG_NONE) continue;
+            newi[ref] = next++;
+            queue.push_back(ref);
+        }
+    }
+    const uint32_t hot = next;
+    for (uint32_t r = 0; r < n; ++r)
+        if (newi[r] == HG_NONE) newi[r] = next++;
+    std::vector<float4> out(rec.size());
+    auto remap = [&](uint32_t ref) { return (ref & HG_LEAF_BIT) || ref >= n ? ref : newi[ref]; };
+    for (uint32_t r = 0; r < n; ++r) {
+        float4* dst = &out[4 * size_t(newi[r])];
+        const float4* src = &rec[4 * size_t(r)];
+        dst[0] = src[0];
+        dst[1] = src[1];
+        dst[2] = src[2];
+        dst[3] = src[3];
+        dst[0].w = bits(remap(ubits(src[0].w)));
+        dst[1].w = bits(remap(ubits(src[1].w)));
+    }
+    rec.swap(out);
+    for (HgDevMesh& m : dm) m.root_ref = remap(m.root_ref);
+    return hot;
+}
+
 int drain_events(hg_ctx* c) {
     if (c->pending.empty() && c->pending_trace.empty()) return HG_OK;
     HG_HIP(c, hipStreamSynchronize(c->stream));
@@ -542,6 +594,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
         return fail(c, HG_E_UNSUPPORTED, "BLAS too large: %zu device node records", rec.size() / 4);
     if (rec.empty()) new_record();
     if (leaf.empty()) leaf.push_back(make_uint2(0, 0));
+    c->hot_records = hot_prefix(rec, dm, HG_NODE_CACHE);
     c->stack_depth = std::max<uint32_t>(2u, (max_depth + 2 + 1) & ~1u);
 
     int rc;
@@ -674,6 +727,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.n_ranks = c->n_ranks;
     kp.n_local_tiles = c->n_local_tiles;
     kp.stack_depth = c->stack_depth;
+    kp.hot_records = c->hot_records;
     // deep BLAS (the dragon: 32 levels) descend in long, uneven runs: let the last few lanes pause while the rest
     // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweeps/sweep28-29.txt)
 
@@ -776,8 +830,10 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             kp.pool = static_cast<float4*>(c->pool.p);
         }
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
-        if (kp.stack_depth > HG_MEGA_LDS_STACK) {  // stack entries beyond the LDS part: one column per thread
-            if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - HG_MEGA_LDS_STACK) * 4)) {
+        // stack entries beyond the LDS part: one column per thread (the streaming kernel's LDS part may be shorter)
+        const uint32_t lds_part = std::min<uint32_t>(HG_MEGA_LDS_STACK, HG_STREAM_LDS_STACK);
+        if (kp.stack_depth > lds_part) {
+            if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - lds_part) * 4)) {
                 c->free_events.push_back(ev);
                 return rc;
             }
