@@ -46,6 +46,7 @@ def write_config(settings: rp.HalogenSettings, camera: rp.Camera, path, frames: 
                  n_spheres: int = 0, n_meshes: int = 0, cubemap_path: str | None = None) -> None:
     lines = [f"width {camera.pixelWidth}", f"height {camera.pixelHeight}", f"fov {_v(camera.fieldOfView)}",
              "position " + " ".join(_v(v) for v in camera.transform.position),
+             "rotation " + " ".join(_v(v) for v in camera.transform.rotation),
              "localToWorld " + " ".join(_v(v) for v in to_unity_floats(camera.transform.local_to_world)),
              f"frames {frames}", f"frame_count {frame_count}", f"n_spheres {n_spheres}", f"n_meshes {n_meshes}"]
     for k in SETTING_KEYS:

@@ -62,7 +62,19 @@ class Camera:
         return float(f32(self.pixelWidth) / f32(self.pixelHeight))
 
     def pose(self):
-        return (self.transform.position_local, self.transform.rotation_local)
+        """What RP:279-293 compares from frame to frame: the WORLD position and rotation (float32)."""
+        return (tuple(float(v) for v in self.transform.position), tuple(float(v) for v in self.transform.rotation))
+
+
+def unity_equals(a, b) -> bool:
+    """Vector3.Equals / Quaternion.Equals (RP:280): componentwise float.Equals, i.e. exact ==, with NaN equal to
+    NaN and +0 equal to -0 (the reference does not use the approximate == operator)."""
+    return len(a) == len(b) and all(x == y or (math.isnan(x) and math.isnan(y)) for x, y in zip(a, b))
+
+
+def camera_moved(prior, pose) -> bool:
+    """RP:279-284: accumulation is cleared when a prior pose exists and its position or rotation differs."""
+    return prior is not None and not (unity_equals(prior[0], pose[0]) and unity_equals(prior[1], pose[1]))
 
 
 def make_params(settings_clamped: dict, camera: Camera, frame_count: int, n_spheres: int, n_meshes: int,
@@ -178,7 +190,7 @@ class HalogenRenderPass:
         identical per-frame semantics (FrameCount advancing, same blend) as long as nothing changes between."""
         self.OnCameraSetup(camera.pixelWidth, camera.pixelHeight)
         pose = camera.pose()
-        if self._prior_pose is not None and pose != self._prior_pose:
+        if camera_moved(self._prior_pose, pose):
             self.ClearAccumulation()
         if self.FrameCount > 1 and not self.s["Accumulate"]:
             self.ClearAccumulation()

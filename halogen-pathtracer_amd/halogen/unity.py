@@ -27,6 +27,16 @@ def quat_to_mat3(q) -> np.ndarray:
     ], dtype=np.float64)
 
 
+def quat_mul(a, b) -> np.ndarray:
+    """Hamilton product a * b of quaternions (x, y, z, w), float64 (Unity's Quaternion * Quaternion)."""
+    ax, ay, az, aw = (float(v) for v in a)
+    bx, by, bz, bw = (float(v) for v in b)
+    return np.array([aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by + ay * bw + az * bx - ax * bz,
+                     aw * bz + az * bw + ax * by - ay * bx,
+                     aw * bw - ax * bx - ay * by - az * bz], dtype=np.float64)
+
+
 def euler_to_quat(ex: float, ey: float, ez: float):
     """Unity Euler angles in degrees (applied Z, then X, then Y) -> quaternion (x, y, z, w)."""
     def axis(ax, deg):
@@ -79,6 +89,16 @@ class Transform:
     def position(self) -> np.ndarray:
         """World position as float32 (Transform.position)."""
         return self.local_to_world[:3, 3].astype(np.float32)
+
+    @property
+    def rotation(self) -> np.ndarray:
+        """World rotation (x, y, z, w) as float32 (Transform.rotation = parent.rotation * localRotation); scale plays
+        no part in it."""
+        q = np.asarray(self.rotation_local, dtype=np.float64)
+        q = q / math.sqrt(float(q @ q))
+        if self.parent is not None:
+            q = quat_mul(self.parent.rotation.astype(np.float64), q)
+        return q.astype(np.float32)
 
 
 # -------------------------------------------------------------------------------------------------

@@ -6,7 +6,7 @@
 // SCENE.hgscene: "HGSCENE1", int32 counts of spheres, meshes, materials, triangles, BVH entries, then the arrays in
 // the reference's struct layouts (44/164/84/72/32 B) — what UpdateObjectBuffers uploads (RP:448-509).
 // CONFIG.txt: one "key value..." per line: the HalogenSettings fields by their reference names, the camera
-// (width, height, fov, position x y z, localToWorld 16 floats in Unity field order), frames, and optionally
+// (width, height, fov, position x y z, rotation x y z w, localToWorld 16 floats in Unity field order), frames, and optionally
 // cubemap PATH ("HGCUBE01", int32 face size, int32 mips, int64 float count, floats).  halogen/host_files.py writes
 // all three from the Python scene description.
 #include <cstdio>
@@ -58,6 +58,9 @@ Config read_config(const std::string& path) {
         else if (k == "height") c.camera.pixelHeight = i();
         else if (k == "fov") c.camera.fieldOfView = f();
         else if (k == "position") { c.camera.position.x = f(); c.camera.position.y = f(); c.camera.position.z = f(); }
+        else if (k == "rotation") {
+            c.camera.rotation.x = f(); c.camera.rotation.y = f(); c.camera.rotation.z = f(); c.camera.rotation.w = f();
+        }
         else if (k == "localToWorld") { for (float& m : c.camera.localToWorld.m) m = f(); }
         else if (k == "frames") c.frames = i();
         else if (k == "frame_count") c.frame_count = i();

@@ -73,11 +73,25 @@ struct HalogenSettings {
 // fieldOfView (degrees, vertical), pixelWidth / pixelHeight, aspect.
 struct Camera {
     hg_mat4 localToWorld{};  // UnityEngine.Matrix4x4 field order (column-major)
-    hg_vec3 position{};
+    hg_vec3 position{};      // transform.position (world)
+    hg_vec4 rotation{0.0f, 0.0f, 0.0f, 1.0f};  // transform.rotation (world quaternion x, y, z, w)
     float fieldOfView = 60.0f;
     int32_t pixelWidth = 256, pixelHeight = 256;
     float aspect() const { return float(pixelWidth) / float(pixelHeight); }
 };
+
+// Vector3.Equals / Quaternion.Equals as RP:280 uses them: componentwise float.Equals, i.e. exact ==, with NaN equal
+// to NaN (and +0 equal to -0).  The reference compares the world position and rotation only, so a scale-only change
+// or a matrix that differs in its bits but not in those does not clear the accumulation.
+inline bool unity_equals(float a, float b) { return a == b || (a != a && b != b); }
+inline bool camera_moved(const hg_vec3& p0, const hg_vec4& r0, const Camera& cam) {  // RP:279-284
+    const hg_vec3& p = cam.position;
+    const hg_vec4& r = cam.rotation;
+    const bool same = unity_equals(p0.x, p.x) && unity_equals(p0.y, p.y) && unity_equals(p0.z, p.z) &&
+                      unity_equals(r0.x, r.x) && unity_equals(r0.y, r.y) && unity_equals(r0.z, r.z) &&
+                      unity_equals(r0.w, r.w);
+    return !same;
+}
 
 // The settings after the constructor's clamping (RP:169-231)
 struct ClampedSettings {
@@ -211,9 +225,10 @@ class HalogenRenderPass {
     // the identical per-frame semantics (FrameCount advancing, the same blend) as long as nothing changes between.
     void Execute(const SceneBuffers& scene, const Camera& camera, int32_t n_frames = 1) {
         OnCameraSetup(camera.pixelWidth, camera.pixelHeight);
-        if (have_pose_ && std::memcmp(&camera.localToWorld, &prior_pose_, sizeof(hg_mat4)) != 0) ClearAccumulation();
+        if (have_pose_ && camera_moved(prior_position_, prior_rotation_, camera)) ClearAccumulation();
         if (FrameCount > 1 && !s_.Accumulate) ClearAccumulation();
-        prior_pose_ = camera.localToWorld;
+        prior_position_ = camera.position;
+        prior_rotation_ = camera.rotation;
         have_pose_ = true;
         if (ObjectBuffersDirty) {
             UpdateObjectBuffers(scene);
@@ -272,7 +287,8 @@ class HalogenRenderPass {
     ClampedSettings s_;
     hg_ctx* ctx_ = nullptr;
     int32_t prior_w_ = -1, prior_h_ = -1;
-    hg_mat4 prior_pose_{};
+    hg_vec3 prior_position_{};  // PriorCameraPosition / PriorCameraRotation (RP:293-294)
+    hg_vec4 prior_rotation_{};
     bool have_pose_ = false;
     int32_t n_spheres_ = 0, n_meshes_ = 0;
     bool cubemap_uploaded_ = false;

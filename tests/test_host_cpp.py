@@ -104,3 +104,65 @@ def test_gpu_cpp_render_pass_matches_golden(gpu, cli, tmp_path, name):
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), name
     for k in ("paths", "rays", "tri_tests", "aabb_tests"):
         assert cnt[k] == meta["counters"][k], (k, cnt[k], meta["counters"][k])
+
+
+# ---- accumulation reset on camera change (RP:279-294): world position and rotation, Vector3/Quaternion.Equals ----
+_PROBE = r"""
+#include <cstdio>
+#include <cstring>
+#include "halogen_render_pass.hpp"
+static float rd() { unsigned u; if (std::scanf("%x", &u) != 1) return 0; float f; std::memcpy(&f, &u, 4); return f; }
+int main() {
+    int n; if (std::scanf("%d", &n) != 1) return 2;
+    for (int i = 0; i < n; ++i) {
+        hg_vec3 p0{rd(), rd(), rd()}; hg_vec4 r0{rd(), rd(), rd(), rd()};
+        halogen::Camera c; c.position = hg_vec3{rd(), rd(), rd()}; c.rotation = hg_vec4{rd(), rd(), rd(), rd()};
+        std::printf("%d\n", halogen::camera_moved(p0, r0, c) ? 1 : 0);
+    }
+    return 0;
+}
+"""
+
+
+def _pose_cases():
+    base = Transform(position=(1.0, 2.0, -3.0), rotation=(0.0, 0.3826834, 0.0, 0.9238795))
+    parent = Transform(position=(0.0, 0.0, 0.0))
+    child = Transform(position=(1.0, 2.0, -3.0), rotation=(0.0, 0.3826834, 0.0, 0.9238795), parent=parent)
+    pose = lambda t: rp.Camera(t).pose()  # noqa: E731
+    p_base = pose(base)
+    yield "same", p_base, pose(Transform(position=(1.0, 2.0, -3.0), rotation=(0.0, 0.3826834, 0.0, 0.9238795))), False
+    yield "scale only", p_base, pose(Transform(position=(1.0, 2.0, -3.0), rotation=(0.0, 0.3826834, 0.0, 0.9238795),
+                                                scale=(2.0, 0.5, 1.0))), False
+    p_child = pose(child)
+    parent.position_local = (0.0, 0.25, 0.0)  # the parent moves: the child's world position changes, local does not
+    yield "parent moved", p_child, pose(child), True
+    parent.position_local = (0.0, 0.0, 0.0)
+    parent.rotation_local = (0.0, 0.0, 0.0998334, 0.9950042)  # the parent turns: world position and rotation change
+    yield "parent turned", p_child, pose(child), True
+    yield "rotation only", p_base, pose(Transform(position=(1.0, 2.0, -3.0), rotation=(0.0, 0.0, 0.0, 1.0))), True
+    z = ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+    yield "-0 equals +0", z, ((-0.0, 0.0, -0.0), (0.0, -0.0, 0.0, 1.0)), False
+    nan = float("nan")
+    yield "NaN equals NaN", ((nan, 1.0, 2.0), z[1]), ((nan, 1.0, 2.0), z[1]), False
+    yield "NaN vs number", ((nan, 1.0, 2.0), z[1]), ((0.0, 1.0, 2.0), z[1]), True
+
+
+def test_camera_reset_rule_matches_reference_in_both_hosts(tmp_path):
+    """the reference clears accumulation when the camera's WORLD position or rotation differs by
+    Equals (RP:279-284); a scale-only change does not, a parent transform change does.  The Python and the C++
+    pass decide identically on the same float32 bits."""
+    src = tmp_path / "probe.cpp"
+    src.write_text(_PROBE)
+    exe = tmp_path / "probe"
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+    cases_ = list(_pose_cases())
+    hexf = lambda v: "%08x" % int(np.float32(v).view(np.uint32))  # noqa: E731
+    lines = [str(len(cases_))]
+    for _, a, b, _ in cases_:
+        lines.append(" ".join(hexf(v) for v in (*a[0], *a[1], *b[0], *b[1])))
+    out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True)
+    cpp = [bool(int(x)) for x in out.stdout.split()]
+    for (name, a, b, want), c in zip(cases_, cpp):
+        assert rp.camera_moved(a, b) == want, name
+        assert c == want, name
+    assert not rp.camera_moved(None, cases_[0][2])
