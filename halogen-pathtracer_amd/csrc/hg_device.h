@@ -336,7 +336,7 @@ __device__ __forceinline__ bool tri_accept(f3 lo, f3 ld, float4 a, float4 b, flo
 // (rare: the BLAS depth cap is 32) spill to a per-lane global column, so the LDS footprint does not cap occupancy.
 // The LDS part is addressed through the address-space-3 array itself (a generic pointer here would turn every
 // access into a flat instruction).
-extern __shared__ uint32_t hg_lds_stack[];
+extern __shared__ __attribute__((aligned(16))) uint32_t hg_lds_stack[];
 template <uint32_t kLds>
 struct Stack {
     uint32_t lane;    // this lane's LDS column
@@ -444,12 +444,22 @@ __device__ __forceinline__ uint32_t next_live_mesh(uint64_t live, uint32_t m, ui
     return r < n ? r : n;
 }
 
+// Streaming kernel's LDS copy of the mesh records (HG_MESH_LDS): mesh m's first HG_MESH_LDS_F4 float4 (w2l columns,
+// header) at float4 index m * HG_MESH_LDS_F4 from word kStreamMeshWord, after the stack rows (hg_mega.hip).
+constexpr uint32_t kStreamMeshWord = (HG_STREAM_CACHE_ROW + HG_NODE_CACHE / 4 + HG_STREAM_LDS_STACK) * 64u;
+template <bool kLds>
+__device__ __forceinline__ float4 mesh_f4(const HgKernelParams& kp, uint32_t m, uint32_t k) {
+    if constexpr (kLds) return reinterpret_cast<const float4*>(hg_lds_stack + kStreamMeshWord)[m * HG_MESH_LDS_F4 + k];
+    else return reinterpret_cast<const float4*>(kp.meshes + m)[k];
+}
+
 // world -> local ray of mesh m, direction NOT normalized (:390-392), its reciprocal and the root ref
+template <bool kLds = false>
 __device__ __forceinline__ void mesh_local_ray(const HgKernelParams& kp, const Ray& ray, uint32_t m, f3& lo, f3& ld,
                                                f3& inv, uint32_t& root) {
-    const float4* md4 = reinterpret_cast<const float4*>(kp.meshes + m);
-    const float4 c0 = md4[0], c1 = md4[1], c2 = md4[2], c3 = md4[3];  // worldToLocal columns
-    root = __float_as_uint(md4[4].x);
+    const float4 c0 = mesh_f4<kLds>(kp, m, 0), c1 = mesh_f4<kLds>(kp, m, 1), c2 = mesh_f4<kLds>(kp, m, 2),
+                 c3 = mesh_f4<kLds>(kp, m, 3);  // worldToLocal columns
+    root = __float_as_uint(mesh_f4<kLds>(kp, m, 4).x);
     lo = mk(((c0.x * ray.o.x + c1.x * ray.o.y) + c2.x * ray.o.z) + c3.x * 1.0f,
             ((c0.y * ray.o.x + c1.y * ray.o.y) + c2.y * ray.o.z) + c3.y * 1.0f,
             ((c0.z * ray.o.x + c1.z * ray.o.y) + c2.z * ray.o.z) + c3.z * 1.0f);
@@ -460,22 +470,24 @@ __device__ __forceinline__ void mesh_local_ray(const HgKernelParams& kp, const R
 }
 
 // Accepted mesh hit (:452-471): interpolated normal x orientation through the inverse-transpose, hit position.
+template <bool kLds = false>
 __device__ __forceinline__ void resolve_mesh(const HgKernelParams& kp, const Ray& ray, float best_t, float best_u,
                                              float best_v, uint32_t best_tri, uint32_t best_mesh, Hit& h) {
-    const HgDevMesh& md = kp.meshes[best_mesh];
     const uint32_t tri = best_tri & 0x7FFFFFFFu;
     const float orient = (best_tri & 0x80000000u) ? -1.0f : 1.0f;
     h.t = best_t;
-    h.mat = md.material;
+    h.mat = __float_as_uint(mesh_f4<kLds>(kp, best_mesh, 4).z);  // HgDevMesh::material
     h.orient = orient;
     const float4 n0 = kp.normals[3 * tri], d1 = kp.normals[3 * tri + 1], d2 = kp.normals[3 * tri + 2];
     f3 n = (xyz(n0) + xyz(d1) * best_u) + xyz(d2) * best_v;
     n = n * orient;
-    // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform)
-    const float* m = md.w2l;
-    f3 w = mk(((n.x * m[0] + n.y * m[1]) + n.z * m[2]) + 0.0f * m[3],
-              ((n.x * m[4] + n.y * m[5]) + n.z * m[6]) + 0.0f * m[7],
-              ((n.x * m[8] + n.y * m[9]) + n.z * m[10]) + 0.0f * m[11]);
+    // mul(float4(n,0), worldToLocal): row vector times matrix (inverse-transpose normal transform); w2l is column-major,
+    // so m[4c + r] = column c, row r and the dot products run down the columns
+    const float4 m0 = mesh_f4<kLds>(kp, best_mesh, 0), m1 = mesh_f4<kLds>(kp, best_mesh, 1),
+                 m2 = mesh_f4<kLds>(kp, best_mesh, 2);
+    f3 w = mk(((n.x * m0.x + n.y * m0.y) + n.z * m0.z) + 0.0f * m0.w,
+              ((n.x * m1.x + n.y * m1.y) + n.z * m1.z) + 0.0f * m1.w,
+              ((n.x * m2.x + n.y * m2.y) + n.z * m2.z) + 0.0f * m2.w);
     h.n = normalize(w);
     h.pos = ray.o + ray.d * best_t;
 }
@@ -851,6 +863,7 @@ struct Trav {
 #endif
 };
 
+template <bool kMeshLds = false>
 __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c) {
     c.rays++;
 #if HG_PHASE_DETAIL == 2
@@ -878,7 +891,7 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     const uint32_t nm = uint32_t(kp.n_meshes);
     t.mi = next_live_mesh(t.live, 0u, nm);
     f3 inv;
-    if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv, t.node);
+    if (t.mi < nm) mesh_local_ray<kMeshLds>(kp, ray, t.mi, t.lo, t.ld, inv, t.node);
 #if HG_PHASE_DETAIL == 2
     if (kp.counters) {
         asm volatile("" : : "v"(t.node), "v"(t.lo.x), "v"(t.ld.x));  // keep the loads' wait inside this phase
@@ -889,7 +902,7 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
 
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
 // leaf, and move to the next live mesh when the current one is exhausted.
-template <class Stk>
+template <bool kMeshLds = false, class Stk>
 __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c,
                                           const Stk& stk, bool act, const LeafShare& ls) {
     // 1/ld (the same rcp_exact values mesh_local_ray computes) is not kept in Trav: live only during this round, it
@@ -1019,7 +1032,7 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         const uint32_t nm = uint32_t(kp.n_meshes);
         t.mi = next_live_mesh(t.live, t.mi + 1u, nm);
         f3 inv_next;
-        if (t.mi < nm) mesh_local_ray(kp, ray, t.mi, t.lo, t.ld, inv_next, t.node);
+        if (t.mi < nm) mesh_local_ray<kMeshLds>(kp, ray, t.mi, t.lo, t.ld, inv_next, t.node);
     }
 #if HG_PHASE_DETAIL == 3
     if (kp.counters) {
@@ -1030,6 +1043,7 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
 }
 
 // The hit get_ray_intersection returns, from a finished traversal (:452-471 and the sphere pass).
+template <bool kMeshLds = false>
 __device__ __forceinline__ Hit trav_hit(const HgKernelParams& kp, const Ray& ray, const Trav& t) {
     Hit h;
     h.t = t.sph_t;
@@ -1038,7 +1052,7 @@ __device__ __forceinline__ Hit trav_hit(const HgKernelParams& kp, const Ray& ray
     h.n = mk(0, 0, 0);
     h.mat = 0;
     if (t.best_t < (t.sph_t - 0.0001f) && t.best_t < kp.far_)
-        resolve_mesh(kp, ray, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, h);
+        resolve_mesh<kMeshLds>(kp, ray, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, h);
     else if (t.sph != HG_NONE)
         resolve_sphere(kp, ray, t.sph, h);
     return h;

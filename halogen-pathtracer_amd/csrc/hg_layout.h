@@ -121,6 +121,17 @@
 #define HG_NODE_CACHE 0  // streaming kernel: the top records of every BLAS (BFS) copied into LDS per wave (records,
 #endif                   // a multiple of 4: 4 records = one 64-lane LDS row)
 #define HG_STREAM_CACHE_ROW 13  // its first LDS row (after the per-lane state rows, hg_mega.hip kRowStack)
+#ifndef HG_MESH_LDS
+#define HG_MESH_LDS 1  // streaming kernel: every mesh's world->local matrix and header (80 B) in the wave's LDS
+#endif                 // when they fit (hg_mesh_lds_fits): the per-lane mesh switch reads LDS, not global memory
+#ifndef HG_STREAM_LDS_PAD
+#define HG_STREAM_LDS_PAD 0  // analysis builds: extra LDS bytes per streaming workgroup (occupancy experiments)
+#endif
+#define HG_MESH_LDS_F4 5  // float4 per cached mesh record: w2l columns 0-3, header (root, tri offset, material, cull)
+// Bytes of LDS per one-wave workgroup that still keep 20 waves (5 per SIMD) on a CU.  Measured, not derived from
+// 160 KiB / 20: 7,424 and 7,472 B run at full occupancy, 7,936 / 7,984 / 8,192 B lose 8-12 % (one wave fewer per
+// CU; tools/sweep_r02_h.txt); 7,680 is the largest multiple of 512 below the first failing size.
+#define HG_WAVE_LDS_BUDGET 7680
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif
@@ -128,7 +139,8 @@
 #define HG_MEGA_LDS_STACK 16  // megakernels: traversal stack entries per lane kept in LDS (deeper ones spill)
 #endif
 #ifndef HG_STREAM_LDS_STACK
-#define HG_STREAM_LDS_STACK HG_MEGA_LDS_STACK  // the same for the streaming kernel
+#define HG_STREAM_LDS_STACK 12  // the same for the streaming kernel (12 and 14 measured equal, 10 equal to 16 without the
+                                // mesh records in LDS; 12 leaves LDS room for 16 meshes, HG_WAVE_LDS_BUDGET)
 #endif
 
 struct alignas(16) HgDevMesh {

@@ -98,6 +98,7 @@ constexpr uint32_t kStreamLdsState = 10;
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
 constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
 static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
+static_assert(kStreamMeshWord == (kRowStack + HG_STREAM_LDS_STACK) * 64u, "mesh records after the full stack rows");
 constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
@@ -428,7 +429,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counte
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
-template <bool kCounters, bool kLdsAcc>
+template <bool kCounters, bool kLdsAcc, bool kMeshLds>
 __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
@@ -449,6 +450,15 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     const LeafShare ls{kRowLeaf * 64u};
     const uint32_t nm = uint32_t(kp.n_meshes);
     constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
+    if (kMeshLds) {  // the wave's copy of the mesh records' first HG_MESH_LDS_F4 float4 (mesh_f4, hg_device.h)
+        float4* mt = reinterpret_cast<float4*>(hg_lds_stack + kStreamMeshWord);
+        const uint32_t nf4 = nm * HG_MESH_LDS_F4;
+        for (uint32_t i = lane; i < nf4; i += 64u) {
+            const uint32_t m = i / HG_MESH_LDS_F4;
+            mt[i] = reinterpret_cast<const float4*>(kp.meshes + m)[i - m * HG_MESH_LDS_F4];
+        }
+        wave_lds_sync();
+    }
 #if HG_NODE_CACHE
     {  // the wave's copy of the hot node records (written before any lane reads it: one wave per workgroup)
         float4* cache = reinterpret_cast<float4*>(hg_lds_stack + kRowCache * 64u);
@@ -482,7 +492,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         s_col.set(mk(0, 0, 0));
         if (lds_acc) s_acc.set(kp.acc[size_t(uint32_t(local_tile)) * 64u + lane]);
         else s_sum.set(mk(0, 0, 0));
-        trav_begin(kp, ray, tv, c);
+        trav_begin<kMeshLds>(kp, ray, tv, c);
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
 #if HG_SHADE_PRIO >= 2
@@ -496,7 +506,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             const uint32_t n_act = uint32_t(__popcll(__ballot(act)));
             if (n_act == 0) break;
             if (n_act <= HG_STREAM_TMIN && __any(work && !act)) break;
-            trav_step(kp, ray, tv, c, stk, act, ls);
+            trav_step<kMeshLds>(kp, ray, tv, c, stk, act, ls);
         }
         if (kCounters) {
             const uint64_t t = wave_clock();
@@ -519,7 +529,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 #if HG_PHASE_DETAIL == 1
             uint64_t tp = kCounters ? wave_clock() : 0;
 #endif
-            const Hit hit = trav_hit(kp, ray, tv);
+            const Hit hit = trav_hit<kMeshLds>(kp, ray, tv);
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 11, tp);
 #endif
@@ -608,7 +618,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 13, tp);
 #endif
-            if (alive) trav_begin(kp, ray, tv, c);
+            if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 14, tp);
 #endif
@@ -642,22 +652,35 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     }
 }
 
+// Bytes of LDS the streaming kernel needs with the mesh records in LDS (0: they do not fit the budget that keeps
+// HG_STREAM_WAVES waves per SIMD, or HG_MESH_LDS is off)
+size_t hg_stream_mesh_lds_bytes(int32_t n_meshes) {
+    if (!HG_MESH_LDS || n_meshes <= 0) return 0;
+    const size_t b = size_t(kStreamMeshWord) * 4u + size_t(n_meshes) * HG_MESH_LDS_F4 * 16u;
+    return b <= HG_WAVE_LDS_BUDGET ? b : 0;
+}
+
+template <bool kCounters, bool kLdsAcc>
+static void launch_stream(const HgKernelParams& kp, uint32_t grid, size_t lds, size_t mesh_lds, hipStream_t stream) {
+    if (mesh_lds)
+        hipLaunchKernelGGL((hg_trace_stream_kernel<kCounters, kLdsAcc, true>), dim3(grid), dim3(64), mesh_lds, stream, kp);
+    else
+        hipLaunchKernelGGL((hg_trace_stream_kernel<kCounters, kLdsAcc, false>), dim3(grid), dim3(64), lds, stream, kp);
+}
+
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
     const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
     if (grid == 0) return hipSuccess;
-    block = 64;
     const uint32_t lds_depth = kp.stack_depth < HG_STREAM_LDS_STACK ? kp.stack_depth : HG_STREAM_LDS_STACK;
-    const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t);
+    const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t) + HG_STREAM_LDS_PAD;
+    const size_t mesh_lds = hg_stream_mesh_lds_bytes(kp.n_meshes);
     const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
-    if (counters && lds_acc)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
-    else if (counters)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
-    else if (lds_acc)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
-    else
-        hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
+    const uint32_t g = uint32_t(grid);
+    if (counters && lds_acc) launch_stream<true, true>(kp, g, lds, mesh_lds, stream);
+    else if (counters) launch_stream<true, false>(kp, g, lds, mesh_lds, stream);
+    else if (lds_acc) launch_stream<false, true>(kp, g, lds, mesh_lds, stream);
+    else launch_stream<false, false>(kp, g, lds, mesh_lds, stream);
     return hipGetLastError();
 }
 
