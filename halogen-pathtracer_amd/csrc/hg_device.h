@@ -444,13 +444,21 @@ __device__ __forceinline__ uint32_t next_live_mesh(uint64_t live, uint32_t m, ui
     return r < n ? r : n;
 }
 
-// Streaming kernel's LDS copy of the mesh records (HG_MESH_LDS): mesh m's first HG_MESH_LDS_F4 float4 (w2l columns,
-// header) at float4 index m * HG_MESH_LDS_F4 from word kStreamMeshWord, after the stack rows (hg_mega.hip).
-constexpr uint32_t kStreamMeshWord = (HG_STREAM_CACHE_ROW + HG_NODE_CACHE / 4 + HG_STREAM_LDS_STACK) * 64u;
+// The wave's LDS copy of the mesh records (HG_MESH_LDS): mesh m's first HG_MESH_LDS_F4 float4 (w2l columns, header)
+// at float4 index m * HG_MESH_LDS_F4 from word kp.mesh_lds_word (after the kernel's stack rows, hg_mega.hip).
 template <bool kLds>
 __device__ __forceinline__ float4 mesh_f4(const HgKernelParams& kp, uint32_t m, uint32_t k) {
-    if constexpr (kLds) return reinterpret_cast<const float4*>(hg_lds_stack + kStreamMeshWord)[m * HG_MESH_LDS_F4 + k];
+    if constexpr (kLds) return reinterpret_cast<const float4*>(hg_lds_stack + kp.mesh_lds_word)[m * HG_MESH_LDS_F4 + k];
     else return reinterpret_cast<const float4*>(kp.meshes + m)[k];
+}
+// copy every mesh record's first HG_MESH_LDS_F4 float4 into the wave's LDS (one wave per workgroup)
+__device__ __forceinline__ void mesh_lds_fill(const HgKernelParams& kp, uint32_t lane) {
+    float4* mt = reinterpret_cast<float4*>(hg_lds_stack + kp.mesh_lds_word);
+    const uint32_t nf4 = uint32_t(kp.n_meshes) * HG_MESH_LDS_F4;
+    for (uint32_t i = lane; i < nf4; i += 64u) {
+        const uint32_t m = i / HG_MESH_LDS_F4;
+        mt[i] = reinterpret_cast<const float4*>(kp.meshes + m)[i - m * HG_MESH_LDS_F4];
+    }
 }
 
 // world -> local ray of mesh m, direction NOT normalized (:390-392), its reciprocal and the root ref
@@ -624,7 +632,7 @@ __device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRa
 // The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
 // the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
 // while-while: all lanes descend inner nodes together until each holds a leaf, then test one leaf each.
-template <class Stk>
+template <bool kMeshLds = false, class Stk>
 __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, const Stk& stk) {
     const float eps = 0.0001f;
     float best_t = h.t;  // closestIntersection.rayT starts at the sphere hit (:381)
@@ -644,7 +652,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     bool active = mi < nm;
     f3 lo = mk(0, 0, 0), ld = mk(0, 0, 0), inv = mk(0, 0, 0);
     uint32_t node = HG_NONE, sp = 0;
-    if (active) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
+    if (active) mesh_local_ray<kMeshLds>(kp, ray, mi, lo, ld, inv, node);
     while (__any(active)) {
 #if HG_TRAV_IFIF
         if (active && !(node & HG_LEAF_BIT)) {  // if-if: one node step per round, leaves tested in the same round
@@ -727,7 +735,7 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         }
         if (active && node == HG_NONE) {  // this mesh is done: the lane's next live mesh
             mi = next_live_mesh(live, mi + 1u, nm);
-            if (mi < nm) mesh_local_ray(kp, ray, mi, lo, ld, inv, node);
+            if (mi < nm) mesh_local_ray<kMeshLds>(kp, ray, mi, lo, ld, inv, node);
             else active = false;
         }
     }
@@ -812,13 +820,13 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
 #endif
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
-        resolve_mesh(kp, ray, best_t, best_u, best_v, best_tri, best_mesh, h);
+        resolve_mesh<kMeshLds>(kp, ray, best_t, best_u, best_v, best_tri, best_mesh, h);
         return true;
     }
     return false;
 }
 
-template <class Stk>
+template <bool kMeshLds = false, class Stk>
 __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ray, Counters& c, const Stk& stk) {  // get_ray_intersection :474-485
     Hit h;
     h.t = HG_INF;
@@ -828,7 +836,7 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
     h.mat = 0;
     c.rays++;
     const uint32_t sph = isect_spheres(kp, ray, h.t);
-    if (!isect_meshes(kp, ray, h, c, stk) && sph != HG_NONE) resolve_sphere(kp, ray, sph, h);
+    if (!isect_meshes<kMeshLds>(kp, ray, h, c, stk) && sph != HG_NONE) resolve_sphere(kp, ray, sph, h);
     return h;
 }
 

@@ -131,7 +131,14 @@
 // Bytes of LDS per one-wave workgroup that still keep 20 waves (5 per SIMD) on a CU.  Measured, not derived from
 // 160 KiB / 20: 7,424 and 7,472 B run at full occupancy, 7,936 / 7,984 / 8,192 B lose 8-12 % (one wave fewer per
 // CU; tools/sweep_r02_h.txt); 7,680 is the largest multiple of 512 below the first failing size.
+#ifndef HG_WAVE_LDS_BUDGET
 #define HG_WAVE_LDS_BUDGET 7680
+#endif
+#ifndef HG_REGEN_LDS_BUDGET
+// The same for the regenerating kernel at its 6 waves per SIMD (24 per CU): 163,840 / 24 = 6,826, less the same
+// reserve; 0 keeps its mesh records in global memory
+#define HG_REGEN_LDS_BUDGET 6144
+#endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif
@@ -187,6 +194,7 @@ struct HgKernelParams {
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
     uint32_t hot_records;  // HG_NODE_CACHE: node records [0, hot_records) are served from the wave's LDS copy
+    uint32_t mesh_lds_word;  // HG_MESH_LDS: LDS word where the wave's copy of the mesh records starts
     uint32_t descent_t;    // relaxed while-while threshold (hg_device.h isect_meshes), 0 = classic while-while
     uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
     uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)

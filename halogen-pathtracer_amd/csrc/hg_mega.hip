@@ -98,7 +98,6 @@ constexpr uint32_t kStreamLdsState = 10;
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
 constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
 static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
-static_assert(kStreamMeshWord == (kRowStack + HG_STREAM_LDS_STACK) * 64u, "mesh records after the full stack rows");
 constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
@@ -223,9 +222,13 @@ hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint
     return hipGetLastError();
 }
 
-template <bool kCounters>
+template <bool kCounters, bool kMeshLds>
 __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
+    if (kMeshLds) {  // the wave's copy of the mesh records (mesh_f4, hg_device.h)
+        mesh_lds_fill(kp, lane);
+        wave_lds_sync();
+    }
     // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
     // one wave per workgroup (launched with 64 threads): wave = workgroup; LDS rows as the streaming kernel's
     const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
 #if HG_REGEN_PRIO
             __builtin_amdgcn_s_setprio(1);
 #endif
-            const Hit hit = intersect(kp, ray, c, stk);
+            const Hit hit = intersect<kMeshLds>(kp, ray, c, stk);
 #if HG_REGEN_PRIO
             __builtin_amdgcn_s_setprio(0);
 #endif
@@ -411,17 +414,28 @@ hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) 
     return hipGetLastError();
 }
 
-hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
+// LDS bytes with the mesh records after `base` bytes of rows, or 0 when they do not fit `budget` (or HG_MESH_LDS is off)
+static size_t mesh_lds_bytes(size_t base, int32_t n_meshes, size_t budget) {
+    if (!HG_MESH_LDS || n_meshes <= 0) return 0;
+    const size_t b = base + size_t(n_meshes) * HG_MESH_LDS_F4 * 16u;
+    return b <= budget ? b : 0;
+}
+
+hipError_t hg_launch_mega_regen(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
     block = 64;
-    const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
+    const int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
     if (grid == 0) return hipSuccess;
-    const uint32_t lds_depth = kp.stack_depth < HG_MEGA_LDS_STACK ? kp.stack_depth : HG_MEGA_LDS_STACK;
+    const uint32_t lds_depth = kp_in.stack_depth < HG_MEGA_LDS_STACK ? kp_in.stack_depth : HG_MEGA_LDS_STACK;
     const size_t lds = size_t(kRegenRowStack + lds_depth) * 64u * sizeof(uint32_t);
-    if (counters)
-        hipLaunchKernelGGL(hg_trace_regen_kernel<true>, dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
-    else
-        hipLaunchKernelGGL(hg_trace_regen_kernel<false>, dim3(uint32_t(grid)), dim3(block), lds, stream, kp);
+    HgKernelParams kp = kp_in;
+    kp.mesh_lds_word = uint32_t(lds / 4u);
+    const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_REGEN_LDS_BUDGET);
+    const dim3 g{uint32_t(grid)}, b{uint32_t(block)};
+    if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_regen_kernel<true, true>), g, b, mesh_lds, stream, kp);
+    else if (counters) hipLaunchKernelGGL((hg_trace_regen_kernel<true, false>), g, b, lds, stream, kp);
+    else if (mesh_lds) hipLaunchKernelGGL((hg_trace_regen_kernel<false, true>), g, b, mesh_lds, stream, kp);
+    else hipLaunchKernelGGL((hg_trace_regen_kernel<false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
 
@@ -450,13 +464,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     const LeafShare ls{kRowLeaf * 64u};
     const uint32_t nm = uint32_t(kp.n_meshes);
     constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
-    if (kMeshLds) {  // the wave's copy of the mesh records' first HG_MESH_LDS_F4 float4 (mesh_f4, hg_device.h)
-        float4* mt = reinterpret_cast<float4*>(hg_lds_stack + kStreamMeshWord);
-        const uint32_t nf4 = nm * HG_MESH_LDS_F4;
-        for (uint32_t i = lane; i < nf4; i += 64u) {
-            const uint32_t m = i / HG_MESH_LDS_F4;
-            mt[i] = reinterpret_cast<const float4*>(kp.meshes + m)[i - m * HG_MESH_LDS_F4];
-        }
+    if (kMeshLds) {  // the wave's copy of the mesh records (mesh_f4, hg_device.h)
+        mesh_lds_fill(kp, lane);
         wave_lds_sync();
     }
 #if HG_NODE_CACHE
@@ -652,14 +661,6 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     }
 }
 
-// Bytes of LDS the streaming kernel needs with the mesh records in LDS (0: they do not fit the budget that keeps
-// HG_STREAM_WAVES waves per SIMD, or HG_MESH_LDS is off)
-size_t hg_stream_mesh_lds_bytes(int32_t n_meshes) {
-    if (!HG_MESH_LDS || n_meshes <= 0) return 0;
-    const size_t b = size_t(kStreamMeshWord) * 4u + size_t(n_meshes) * HG_MESH_LDS_F4 * 16u;
-    return b <= HG_WAVE_LDS_BUDGET ? b : 0;
-}
-
 template <bool kCounters, bool kLdsAcc>
 static void launch_stream(const HgKernelParams& kp, uint32_t grid, size_t lds, size_t mesh_lds, hipStream_t stream) {
     if (mesh_lds)
@@ -668,13 +669,15 @@ static void launch_stream(const HgKernelParams& kp, uint32_t grid, size_t lds, s
         hipLaunchKernelGGL((hg_trace_stream_kernel<kCounters, kLdsAcc, false>), dim3(grid), dim3(64), lds, stream, kp);
 }
 
-hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream) {
+hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
-    const int64_t grid = int64_t(kp.n_local_tiles) * kp.frame_split;
+    const int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
     if (grid == 0) return hipSuccess;
-    const uint32_t lds_depth = kp.stack_depth < HG_STREAM_LDS_STACK ? kp.stack_depth : HG_STREAM_LDS_STACK;
+    const uint32_t lds_depth = kp_in.stack_depth < HG_STREAM_LDS_STACK ? kp_in.stack_depth : HG_STREAM_LDS_STACK;
     const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t) + HG_STREAM_LDS_PAD;
-    const size_t mesh_lds = hg_stream_mesh_lds_bytes(kp.n_meshes);
+    HgKernelParams kp = kp_in;
+    kp.mesh_lds_word = uint32_t(lds / 4u);
+    const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
     const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
     const uint32_t g = uint32_t(grid);
     if (counters && lds_acc) launch_stream<true, true>(kp, g, lds, mesh_lds, stream);
