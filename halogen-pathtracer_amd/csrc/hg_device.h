@@ -141,6 +141,10 @@ __device__ __forceinline__ uint64_t phase_mark(const HgKernelParams& kp, int slo
         atomicAdd(kp.counters + slot, (unsigned long long)(t - since));
     return wave_clock();
 }
+// 64-lane ballot of a bool straight from the compare mask (the HIP __ballot(int) materialises the predicate in a
+// VGPR and compares it again)
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t wave_count(bool p) { return uint32_t(__builtin_popcountll(wave_ballot(p))); }
 __device__ __forceinline__ uint32_t wave_once() {
     return __lane_id() == uint32_t(__builtin_ctzll(__ballot(1))) ? 1u : 0u;
 }
@@ -661,12 +665,13 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         // lane is at a leaf), and in any case until at least one lane can make other progress (a leaf to test or
         // its mesh finished); the few stragglers pause while the others test their leaves.  Each lane's own
         // sequence of node / leaf steps is unchanged.
-        for (;;) {
-            const uint32_t n_desc = uint32_t(__popcll(__ballot(active && !(node & HG_LEAF_BIT))));
-            if (n_desc == 0u) break;
-            if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(active)))) break;
+        const uint64_t act_mask = wave_ballot(active);
+        const uint32_t dt = kp.descent_t;
+        for (uint64_t dm = act_mask & wave_ballot(int32_t(node) >= 0);
+             dm != 0ull && (uint32_t(__builtin_popcountll(dm)) > dt || dm == act_mask);
+             dm = act_mask & wave_ballot(int32_t(node) >= 0)) {
             c.node_rounds += wave_once();
-            if (active && !(node & HG_LEAF_BIT)) {
+            if (active && int32_t(node) >= 0) {
 #endif
                 const uint32_t ro = node << 6;
                 const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
@@ -919,12 +924,14 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
 #if HG_PHASE_DETAIL == 3
     uint64_t tp = kp.counters ? wave_clock() : 0;
 #endif
-    for (;;) {  // relaxed while-while, as in isect_meshes
-        const uint32_t n_desc = uint32_t(__popcll(__ballot(act && !(t.node & HG_LEAF_BIT))));
-        if (n_desc == 0u) break;
-        if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(act)))) break;
+    const uint64_t act_mask = wave_ballot(act);  // act is fixed for the round
+    const uint32_t dt = kp.descent_t;
+    // lanes at an inner node (HG_NONE has the leaf bit): the wave descends while more than dt of them are left, or
+    // while every active lane is still descending (relaxed while-while, as in isect_meshes)
+    uint64_t dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
+    while (dm != 0ull && (uint32_t(__builtin_popcountll(dm)) > dt || dm == act_mask)) {
         c.node_rounds += wave_once();
-        if (act && !(t.node & HG_LEAF_BIT)) {
+        if (act && int32_t(t.node) >= 0) {
 #if HG_NODE_CACHE
             // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
             float4 a_lo, a_hi, b_lo, b_hi;
@@ -968,6 +975,7 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
 #endif
         }
+        dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     }
 #if HG_PHASE_DETAIL == 3
     if (kp.counters) tp = phase_mark(kp, 11, tp);

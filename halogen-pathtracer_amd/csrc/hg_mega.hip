@@ -512,9 +512,9 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         if (kCounters) cyc_trav -= wave_clock();
         for (;;) {
             const bool act = work && tv.mi < nm;
-            const uint32_t n_act = uint32_t(__popcll(__ballot(act)));
-            if (n_act == 0) break;
-            if (n_act <= HG_STREAM_TMIN && __any(work && !act)) break;
+            const uint64_t am = wave_ballot(act);
+            // (work includes act: some lane waits to shade iff the work mask differs)
+            if (am == 0ull || (uint32_t(__builtin_popcountll(am)) <= HG_STREAM_TMIN && wave_ballot(work) != am)) break;
             trav_step<kMeshLds>(kp, ray, tv, c, stk, act, ls);
         }
         if (kCounters) {
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         // (rays that finish at once — everything culled — shade again in this loop while at least
         // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
         for (uint32_t it = 0;; ++it) {
-            const uint32_t n_sh = uint32_t(__popcll(__ballot(work && tv.mi >= nm)));
+            const uint32_t n_sh = wave_count(work && tv.mi >= nm);
             if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
             if (!(work && tv.mi >= nm)) continue;
             c.shade_rounds += wave_once();
