@@ -319,6 +319,9 @@ __device__ __forceinline__ uint64_t mesh_live_mask(const HgKernelParams& kp, f3 
 
 // Triangle test of triangle_intersection_doublesided (:307-355) with every term computed and one combined accept
 // (same values as the early-out form).  Returns true when the hit is accepted as the new closest (:416).
+// kFlat (the distributed leaf test, measured: stream C3 +0.7 %; the regenerating kernel's sequential loop loses
+// 1.5-3 % with it, tools/sweeps/NOTES_r02.md) evaluates the accept without short-circuit branches.
+template <bool kFlat = false>
 __device__ __forceinline__ bool tri_accept(f3 lo, f3 ld, float4 a, float4 b, float cz, float best_t, float& t,
                                            float& U, float& V, bool& front) {
     const f3 e1 = mk(a.w, b.x, b.y);
@@ -332,6 +335,9 @@ __device__ __forceinline__ bool tri_accept(f3 lo, f3 ld, float4 a, float4 b, flo
     V = dot(ld, qvec) * inv_det;
     t = dot(e2, qvec) * inv_det;
     front = det > 0.0f;
+    if (kFlat)  // bitwise & of the conditions: one straight compare chain instead of a branch per short-circuit step
+        return bool(int(!(fabsf(det) < 0.00000001f)) & int(!(U < 0.0f || U > 1.0f)) & int(!(V < 0.0f || U + V > 1.0f)) &
+                    int(t > 0.0f) & int(t > 0.0001f) & int(t < best_t));
     return !(fabsf(det) < 0.00000001f) && !(U < 0.0f || U > 1.0f) && !(V < 0.0f || U + V > 1.0f) && t > 0.0f &&
            t > 0.0001f && t < best_t;
 }
@@ -608,7 +614,7 @@ __device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRa
             const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
             const float cz = ld_off(kp.tri_c, ti << 2);
             c.tri++;
-            acc = tri_accept(olo, old, a, b, cz, obt, tt, U, V, front);
+            acc = tri_accept<true>(olo, old, a, b, cz, obt, tt, U, V, front);
         }
         wave_lds_sync();
         if (acc) atomicMin(ls.key(o), (static_cast<unsigned long long>(__float_as_uint(tt)) << 32) | ti);
