@@ -139,6 +139,9 @@
 // reserve; 0 keeps its mesh records in global memory
 #define HG_REGEN_LDS_BUDGET 6144
 #endif
+#ifndef HG_STREAM_ITEMS
+#define HG_STREAM_ITEMS 1  // streaming kernel: lanes take (pixel, frame) items of the wave's tile (frame colours blended after)
+#endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif

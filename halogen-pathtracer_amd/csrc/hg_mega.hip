@@ -494,6 +494,45 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     float acc_rough = 0.0f;
     Trav tv;
     tv.mi = nm;
+#if HG_STREAM_ITEMS
+    // The wave's work is its tile's (pixel, frame) items: with v pixels of the tile inside the image (a w x h
+    // rectangle, 64 inside the image), item k is valid pixel k mod v of frame f_begin + k / v.  Lane l starts with
+    // item l; a lane whose frame is done takes the next unassigned item (a wave-wide rank), so the lanes stay busy
+    // until the tile's items run out instead of each waiting for its own pixel's slowest frames.  Every frame's
+    // colour goes to frame_color and hg_blend_frames applies the accumulation blend in frame order.
+    // (wave-uniform values pinned to scalar registers)
+    const int gtile0 = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
+    const uint32_t tx0 = uint32_t(gtile0 % kp.tiles_x) * HG_TILE, ty0 = uint32_t(gtile0 / kp.tiles_x) * HG_TILE;
+    const uint32_t tw = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0)));
+    const uint32_t th = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0)));
+    const uint32_t nv = tw * th;
+    const uint32_t n_items =
+        __builtin_amdgcn_readfirstlane((chunk < split && f_end > f_begin) ? nv * (f_end - f_begin) : 0u);
+    uint32_t next_k = 64u;  // items handed out (wave-uniform)
+    uint32_t pix = lane;    // the item's pixel within the tile (x + 8 y)
+    // item k -> (pixel, frame offset): shifts for a whole tile, divisions only at the image edge
+    auto item = [nv, tw](uint32_t k, uint32_t& p, uint32_t& q) {
+        if (nv == 64u) {
+            p = k & 63u;
+            q = k >> 6;
+        } else {
+            q = k / nv;
+            const uint32_t i = k - q * nv;
+            p = (i % tw) + 8u * (i / tw);
+        }
+    };
+    if (lane < n_items) {   // item `lane`
+        uint32_t q;
+        item(lane, pix, q);
+        px = tx0 + (pix & 7u);
+        py = ty0 + (pix >> 3);
+        fs = (f_begin + q) << 16;
+        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f_begin + q : 1u, pcg_hash(px + py * kp.Wu), 0u};
+    }
+    work = lane < n_items;
+#else
+    const uint32_t pix = lane;
+#endif
     if (work) {
         ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
@@ -533,7 +572,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         for (uint32_t it = 0;; ++it) {
             const uint32_t n_sh = wave_count(work && tv.mi >= nm);
             if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
-            if (!(work && tv.mi >= nm)) continue;
+            bool need = false;  // HG_STREAM_ITEMS: this lane's frame is done, it takes the next item
+            if (work && tv.mi >= nm) {
             c.shade_rounds += wave_once();
 #if HG_PHASE_DETAIL == 1
             uint64_t tp = kCounters ? wave_clock() : 0;
@@ -578,8 +618,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + lane;
-                    if (split > 1u) {  // frame-parallel: this frame's colour, blended later in frame order
+                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
+                    if (HG_STREAM_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
                         kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
@@ -596,7 +636,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                         else kp.acc[slot_i] = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
+                    need = HG_STREAM_ITEMS;
+                    if (!HG_STREAM_ITEMS && (fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
@@ -608,8 +649,8 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                 if (next) {
                     {
                         const int gtile = kp.rank + local_tile * kp.n_ranks;
-                        const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-                        const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+                        const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (pix & 7u);
+                        const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (pix >> 3);
                         ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     }
                     thr = mk(1, 1, 1);
@@ -618,7 +659,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                     bounce = 0;
                     paths++;
                     alive = true;
-                } else {
+                } else if (!need) {
                     work = false;
                 }
             }
@@ -630,6 +671,36 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 14, tp);
+#endif
+            }
+#if HG_STREAM_ITEMS
+            const uint64_t needm = wave_ballot(need);
+            if (needm) {  // lanes whose frame is done take the next items, in lane order
+                const uint32_t k = next_k + __builtin_amdgcn_mbcnt_hi(uint32_t(needm >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo(uint32_t(needm), 0u));
+                next_k += uint32_t(__builtin_popcountll(needm));
+                if (need) {
+                    if (k < n_items) {
+                        uint32_t q;
+                        item(k, pix, q);
+                        const uint32_t f = f_begin + q;
+                        const uint32_t qx = tx0 + (pix & 7u), qy = ty0 + (pix >> 3);
+                        fs = f << 16;
+                        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
+                        ms = MediumStack{0ull, 0};
+                        ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                        s_thr.set(mk(1, 1, 1));
+                        s_col.set(mk(0, 0, 0));
+                        s_sum.set(mk(0, 0, 0));
+                        acc_rough = 0.0f;
+                        bounce = 0;
+                        paths++;
+                        trav_begin<kMeshLds>(kp, ray, tv, c);
+                    } else {
+                        work = false;
+                    }
+                }
+            }
 #endif
         }
 #if HG_SHADE_PRIO == 1
@@ -678,7 +749,7 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     HgKernelParams kp = kp_in;
     kp.mesh_lds_word = uint32_t(lds / 4u);
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
-    const bool lds_acc = HG_LDS_ACC && kp.spp == 1u && kp.frame_split == 1;
+    const bool lds_acc = HG_LDS_ACC && !HG_STREAM_ITEMS && kp.spp == 1u && kp.frame_split == 1;
     const uint32_t g = uint32_t(grid);
     if (counters && lds_acc) launch_stream<true, true>(kp, g, lds, mesh_lds, stream);
     else if (counters) launch_stream<true, false>(kp, g, lds, mesh_lds, stream);
