@@ -146,6 +146,50 @@ __device__ __forceinline__ void record_tile_cost(uint32_t lane) {
     if (p) atomicAdd(p, (unsigned long long)(wave_clock() - hg_wave_t0[threadIdx.x >> 6]));
 }
 
+// (pixel, frame) items of a wave's tile (HG_STREAM_ITEMS / HG_REGEN_ITEMS): with the v pixels of the tile inside the
+// image (a w x h rectangle; all 64 for a whole tile), item k is valid pixel k mod v of frame f_begin + k / v.  Lane l
+// starts with item l; a lane whose frame is done takes the next unassigned item (its rank among the wave's lanes that
+// need one), so the lanes stay busy until the tile's items run out instead of each waiting for its own pixel's
+// slowest frames.  Every frame's colour goes to frame_color and hg_blend_frames applies the accumulation blend in
+// frame order afterwards: the same operations in the same order as a lane tracing its pixel's frames in turn.
+struct TileItems {
+    uint32_t tx0, ty0, tw, nv, n_items, f_begin;  // wave-uniform (scalar registers)
+    uint32_t next_k;                               // items handed out
+    __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe) {
+        const int g = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
+        tx0 = uint32_t(g % kp.tiles_x) * HG_TILE;
+        ty0 = uint32_t(g / kp.tiles_x) * HG_TILE;
+        tw = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0)));
+        const uint32_t th = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0)));
+        nv = tw * th;
+        n_items = __builtin_amdgcn_readfirstlane(valid && fe > fb ? nv * (fe - fb) : 0u);
+        f_begin = fb;
+        next_k = 64u;
+    }
+    // item k -> its pixel within the tile (x + 8 y) and its frame: shifts for a whole tile, divisions at the edge
+    __device__ __forceinline__ void get(uint32_t k, uint32_t& pix, uint32_t& frame) const {
+        uint32_t q;
+        if (nv == 64u) {
+            pix = k & 63u;
+            q = k >> 6;
+        } else {
+            q = k / nv;
+            const uint32_t i = k - q * nv;
+            pix = (i % tw) + 8u * (i / tw);
+        }
+        frame = f_begin + q;
+    }
+    // every lane calls this (top level): lanes with `need` get the next items in lane order; false: no item is left
+    __device__ __forceinline__ bool take(bool need, uint32_t& pix, uint32_t& frame) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(need);
+        const uint32_t k = next_k + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        next_k += uint32_t(__builtin_popcountll(m));
+        if (!need || k >= n_items) return false;
+        get(k, pix, frame);
+        return true;
+    }
+};
+
 // One workgroup of 1024 threads: tile_order = the local tiles by descending cost, STABLE (equal buckets keep
 // tile-index order, so the dispatch order of a launch is a deterministic function of the recorded costs), then the
 // costs are cleared for the next launch.  Counting sort over 1024 linear cost buckets (bucket 0 = most expensive):
@@ -259,6 +303,21 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     MediumStack ms{0ull, 0};
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
     float acc_rough = 0.0f;
+#if HG_REGEN_ITEMS
+    TileItems items(kp, local_tile, chunk < split, f_begin, f_end);
+    uint32_t pix = lane;  // the item's pixel within the tile (x + 8 y)
+    if (lane < items.n_items) {  // item `lane`
+        uint32_t f;
+        items.get(lane, pix, f);
+        px = items.tx0 + (pix & 7u);
+        py = items.ty0 + (pix >> 3);
+        fs = f << 16;
+        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
+    }
+    work = lane < items.n_items;
+#else
+    const uint32_t pix = lane;
+#endif
     if (work) {
         ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
         paths++;
@@ -271,6 +330,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         const uint64_t t0 = kCounters ? wave_clock() : 0;
         const bool was_work = work;
         uint64_t t1 = 0;
+        bool need = false;  // HG_REGEN_ITEMS: this lane's frame is done, it takes the next item
         if (work) {
 #if HG_REGEN_PRIO
             __builtin_amdgcn_s_setprio(1);
@@ -313,8 +373,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 if (!next) {
                     const float sppf = float(kp.spp);
                     const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
-                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + lane;
-                    if (split > 1u) {  // frame-parallel: this frame's colour, blended later in frame order
+                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
+                    if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
                         kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
@@ -331,7 +391,8 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                         *slot = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
+                    need = HG_REGEN_ITEMS;
+                    if (!HG_REGEN_ITEMS && (fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
@@ -342,21 +403,41 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                 s_sum.set(sum);
                 if (next) {
                     const int gtile = kp.rank + local_tile * kp.n_ranks;
-                    const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-                    const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
+                    const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (pix & 7u);
+                    const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (pix >> 3);
                     ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     thr = mk(1, 1, 1);
                     col = mk(0, 0, 0);
                     acc_rough = 0.0f;
                     bounce = 0;
                     paths++;
-                } else {
+                } else if (!need) {
                     work = false;
                 }
             }
             s_thr.set(thr);
             s_col.set(col);
         }
+#if HG_REGEN_ITEMS
+        if (wave_ballot(need)) {  // lanes whose frame is done take the next items
+            uint32_t f = 0;
+            if (items.take(need, pix, f)) {
+                const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
+                fs = f << 16;
+                smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
+                ms = MediumStack{0ull, 0};
+                ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                s_thr.set(mk(1, 1, 1));
+                s_col.set(mk(0, 0, 0));
+                s_sum.set(mk(0, 0, 0));
+                acc_rough = 0.0f;
+                bounce = 0;
+                paths++;
+            } else if (need) {
+                work = false;
+            }
+        }
+#endif
         if (kCounters) {  // t1 was read inside the divergent branch: take it from a lane that ran it
             const uint64_t t2 = wave_clock();
             const int src = __ffsll((unsigned long long)__ballot(was_work)) - 1;
@@ -495,41 +576,17 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     Trav tv;
     tv.mi = nm;
 #if HG_STREAM_ITEMS
-    // The wave's work is its tile's (pixel, frame) items: with v pixels of the tile inside the image (a w x h
-    // rectangle, 64 inside the image), item k is valid pixel k mod v of frame f_begin + k / v.  Lane l starts with
-    // item l; a lane whose frame is done takes the next unassigned item (a wave-wide rank), so the lanes stay busy
-    // until the tile's items run out instead of each waiting for its own pixel's slowest frames.  Every frame's
-    // colour goes to frame_color and hg_blend_frames applies the accumulation blend in frame order.
-    // (wave-uniform values pinned to scalar registers)
-    const int gtile0 = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
-    const uint32_t tx0 = uint32_t(gtile0 % kp.tiles_x) * HG_TILE, ty0 = uint32_t(gtile0 / kp.tiles_x) * HG_TILE;
-    const uint32_t tw = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0)));
-    const uint32_t th = __builtin_amdgcn_readfirstlane(min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0)));
-    const uint32_t nv = tw * th;
-    const uint32_t n_items =
-        __builtin_amdgcn_readfirstlane((chunk < split && f_end > f_begin) ? nv * (f_end - f_begin) : 0u);
-    uint32_t next_k = 64u;  // items handed out (wave-uniform)
-    uint32_t pix = lane;    // the item's pixel within the tile (x + 8 y)
-    // item k -> (pixel, frame offset): shifts for a whole tile, divisions only at the image edge
-    auto item = [nv, tw](uint32_t k, uint32_t& p, uint32_t& q) {
-        if (nv == 64u) {
-            p = k & 63u;
-            q = k >> 6;
-        } else {
-            q = k / nv;
-            const uint32_t i = k - q * nv;
-            p = (i % tw) + 8u * (i / tw);
-        }
-    };
-    if (lane < n_items) {   // item `lane`
-        uint32_t q;
-        item(lane, pix, q);
-        px = tx0 + (pix & 7u);
-        py = ty0 + (pix >> 3);
-        fs = (f_begin + q) << 16;
-        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f_begin + q : 1u, pcg_hash(px + py * kp.Wu), 0u};
+    TileItems items(kp, local_tile, chunk < split, f_begin, f_end);
+    uint32_t pix = lane;  // the item's pixel within the tile (x + 8 y)
+    if (lane < items.n_items) {  // item `lane`
+        uint32_t f;
+        items.get(lane, pix, f);
+        px = items.tx0 + (pix & 7u);
+        py = items.ty0 + (pix >> 3);
+        fs = f << 16;
+        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
     }
-    work = lane < n_items;
+    work = lane < items.n_items;
 #else
     const uint32_t pix = lane;
 #endif
@@ -674,31 +731,23 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
 #endif
             }
 #if HG_STREAM_ITEMS
-            const uint64_t needm = wave_ballot(need);
-            if (needm) {  // lanes whose frame is done take the next items, in lane order
-                const uint32_t k = next_k + __builtin_amdgcn_mbcnt_hi(uint32_t(needm >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo(uint32_t(needm), 0u));
-                next_k += uint32_t(__builtin_popcountll(needm));
-                if (need) {
-                    if (k < n_items) {
-                        uint32_t q;
-                        item(k, pix, q);
-                        const uint32_t f = f_begin + q;
-                        const uint32_t qx = tx0 + (pix & 7u), qy = ty0 + (pix >> 3);
-                        fs = f << 16;
-                        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
-                        ms = MediumStack{0ull, 0};
-                        ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
-                        s_thr.set(mk(1, 1, 1));
-                        s_col.set(mk(0, 0, 0));
-                        s_sum.set(mk(0, 0, 0));
-                        acc_rough = 0.0f;
-                        bounce = 0;
-                        paths++;
-                        trav_begin<kMeshLds>(kp, ray, tv, c);
-                    } else {
-                        work = false;
-                    }
+            if (wave_ballot(need)) {  // lanes whose frame is done take the next items
+                uint32_t f = 0;
+                if (items.take(need, pix, f)) {
+                    const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
+                    fs = f << 16;
+                    smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
+                    ms = MediumStack{0ull, 0};
+                    ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                    s_thr.set(mk(1, 1, 1));
+                    s_col.set(mk(0, 0, 0));
+                    s_sum.set(mk(0, 0, 0));
+                    acc_rough = 0.0f;
+                    bounce = 0;
+                    paths++;
+                    trav_begin<kMeshLds>(kp, ray, tv, c);
+                } else if (need) {
+                    work = false;
                 }
             }
 #endif

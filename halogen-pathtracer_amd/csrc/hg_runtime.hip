@@ -813,7 +813,9 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         }
         if (units > 0) split = int(std::min<int64_t>(split, kMaxWaves / units));
         int chunk_max = HG_REGEN_MAX_CHUNK;
-        const bool colours = split > 1 || (stream_k && HG_STREAM_ITEMS);  // frame colours, blended after the launch
+        // frame colours, blended after the launch (frame split, or item scheduling)
+        const bool items_k = regen && !pool_k && (stream_k ? HG_STREAM_ITEMS : HG_REGEN_ITEMS);
+        const bool colours = split > 1 || items_k;
         if (colours) {
             const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
             chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
@@ -880,7 +882,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
                     : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
                                : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
-                if (e == hipSuccess && (kc.frame_split > 1 || (stream_k && HG_STREAM_ITEMS)))
+                if (e == hipSuccess && (kc.frame_split > 1 || items_k))
                     e = hg_launch_blend_frames(kc, c->stream);
                 done += kc.n_frames;
             }
