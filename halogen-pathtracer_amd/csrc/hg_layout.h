@@ -52,7 +52,8 @@
 #define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~120 VGPRs)
 #endif
 #ifndef HG_STREAM_TMIN
-#define HG_STREAM_TMIN 12  // streaming kernel: shade once at most this many lanes are still traversing (tools/sweeps/sweep54.txt)
+#define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing (12 before the
+                           // item scheduling, tools/sweeps/sweep54.txt; 16 with it, +1.1 %, tools/sweep_r02_ac.txt)
 #endif
 #ifndef HG_RCP_NORMALIZE
 #define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)
