@@ -220,6 +220,14 @@ __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
+// Triangle ti's Moller-Trumbore operands from the three SoA streams: a = (v0, e1.x), b = (e1.yz, e2.xy), cz = e2.z.
+// (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md.)
+__device__ __forceinline__ void tri_load(const HgKernelParams& kp, uint32_t ti, float4& a, float4& b, float& cz) {
+    a = ld_off(kp.tri_a, ti << 4);
+    b = ld_off(kp.tri_b, ti << 4);
+    cz = ld_off(kp.tri_c, ti << 2);
+}
+
 // Load of scene data the kernel never writes (mesh records, spheres) through the constant address space: a
 // wave-uniform address then compiles to a scalar load (s_load_dwordx4, scalar cache) even after the kernel's own
 // global stores, where a generic load must stay a vector load (one full memory latency per mesh / sphere).
@@ -611,8 +619,9 @@ __device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRa
         float tt = 0.0f, U = 0.0f, V = 0.0f;
         bool front = false;
         if (base + lane < total) {
-            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-            const float cz = ld_off(kp.tri_c, ti << 2);
+            float4 a, b;
+            float cz;
+            tri_load(kp, ti, a, b, cz);
             c.tri++;
             acc = tri_accept<true>(olo, old, a, b, cz, obt, tt, U, V, front);
         }
@@ -715,8 +724,9 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             const uint2 leaf = leaf_range(kp, node);
             const uint32_t end = leaf.x + leaf.y;
 #if HG_TRI_PREFETCH
-            float4 na = ld_off(kp.tri_a, leaf.x << 4), nb = ld_off(kp.tri_b, leaf.x << 4);
-            float nc = ld_off(kp.tri_c, leaf.x << 2);
+            float4 na, nb;
+            float nc;
+            tri_load(kp, leaf.x, na, nb, nc);
 #endif
             for (uint32_t ti = leaf.x; ti < end; ++ti) {
                 c.tri_rounds += wave_once();
@@ -724,12 +734,11 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 const float4 a = na, b = nb;
                 const float cz = nc;
                 const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
-                na = ld_off(kp.tri_a, tn << 4);
-                nb = ld_off(kp.tri_b, tn << 4);
-                nc = ld_off(kp.tri_c, tn << 2);
+                tri_load(kp, tn, na, nb, nc);
 #else
-                const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-                const float cz = ld_off(kp.tri_c, ti << 2);
+                float4 a, b;
+                float cz;
+                tri_load(kp, ti, a, b, cz);
 #endif
                 c.tri++;
                 float t, U, V;
@@ -796,21 +805,21 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 uint32_t ti = leaf.x;
                 const uint32_t end = leaf.x + leaf.y;
 #if HG_TRI_PREFETCH
-                float4 ta = ld_off(kp.tri_a, ti << 4), tb = ld_off(kp.tri_b, ti << 4);
-                float tc = ld_off(kp.tri_c, ti << 2);
+                float4 ta, tb;
+                float tc;
+                tri_load(kp, ti, ta, tb, tc);
 #endif
                 for (; ti < end; ++ti) {
 #if HG_TRI_PREFETCH
                     const float4 a = ta, b = tb;
                     const float cz = tc;
                     if (ti + 1 < end) {
-                        ta = ld_off(kp.tri_a, (ti + 1) << 4);
-                        tb = ld_off(kp.tri_b, (ti + 1) << 4);
-                        tc = ld_off(kp.tri_c, (ti + 1) << 2);
+                        tri_load(kp, ti + 1, ta, tb, tc);
                     }
 #else
-                    const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-                    const float cz = ld_off(kp.tri_c, ti << 2);
+                    float4 a, b;
+                    float cz;
+                    tri_load(kp, ti, a, b, cz);
 #endif
                     c.tri++;
                     float t, U, V;
@@ -1012,8 +1021,9 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
 #if HG_STREAM_TRI_PREFETCH
-        float4 na = ld_off(kp.tri_a, leaf.x << 4), nb = ld_off(kp.tri_b, leaf.x << 4);
-        float nc = ld_off(kp.tri_c, leaf.x << 2);
+        float4 na, nb;
+        float nc;
+        tri_load(kp, leaf.x, na, nb, nc);
 #endif
         for (uint32_t ti = leaf.x; ti < end; ++ti) {
             c.tri_rounds += wave_once();
@@ -1021,12 +1031,11 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             const float4 a = na, b = nb;
             const float cz = nc;
             const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
-            na = ld_off(kp.tri_a, tn << 4);
-            nb = ld_off(kp.tri_b, tn << 4);
-            nc = ld_off(kp.tri_c, tn << 2);
+            tri_load(kp, tn, na, nb, nc);
 #else
-            const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-            const float cz = ld_off(kp.tri_c, ti << 2);
+            float4 a, b;
+            float cz;
+            tri_load(kp, ti, a, b, cz);
 #endif
             c.tri++;
             float tt, U, V;

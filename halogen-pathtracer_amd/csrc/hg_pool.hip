@@ -206,8 +206,9 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                     const uint32_t end = leaf.x + leaf.y;
                     for (uint32_t ti = leaf.x; ti < end; ++ti) {
                         c.tri_rounds += wave_once();
-                        const float4 a = ld_off(kp.tri_a, ti << 4), b = ld_off(kp.tri_b, ti << 4);
-                        const float cz = ld_off(kp.tri_c, ti << 2);
+                        float4 a, b;
+                        float cz;
+                        tri_load(kp, ti, a, b, cz);
                         c.tri++;
                         float tt, U, V;
                         bool front;

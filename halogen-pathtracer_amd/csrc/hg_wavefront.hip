@@ -285,15 +285,14 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
             const uint2 leaf = leaf_range(kp, node);
             uint32_t ti = leaf.x;
             const uint32_t end = leaf.x + leaf.y;
-            float4 ta = kp.tri_a[ti], tb = kp.tri_b[ti];
-            float tc = kp.tri_c[ti];
+            float4 ta, tb;
+            float tc;
+            tri_load(kp, ti, ta, tb, tc);
             for (; ti < end; ++ti) {
                 const float4 a = ta, b = tb;
                 const float cz = tc;
                 if (ti + 1 < end) {
-                    ta = kp.tri_a[ti + 1];
-                    tb = kp.tri_b[ti + 1];
-                    tc = kp.tri_c[ti + 1];
+                    tri_load(kp, ti + 1, ta, tb, tc);
                 }
                 c_tri++;
                 // triangle_intersection_doublesided :307-355 (all terms computed, one combined accept)
