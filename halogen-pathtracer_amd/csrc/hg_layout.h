@@ -144,7 +144,7 @@
 #define HG_STREAM_ITEMS 1  // streaming kernel: lanes take (pixel, frame) items of the wave's tile (frame colours blended after)
 #endif
 #ifndef HG_REGEN_ITEMS
-#define HG_REGEN_ITEMS 0  // regenerating kernel: the same (pixel, frame) item scheduling (HG_STREAM_ITEMS)
+#define HG_REGEN_ITEMS 1  // regenerating kernel: the same (pixel, frame) item scheduling (HG_STREAM_ITEMS)
 #endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)

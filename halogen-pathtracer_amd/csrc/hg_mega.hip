@@ -152,10 +152,10 @@ __device__ __forceinline__ void record_tile_cost(uint32_t lane) {
 // need one), so the lanes stay busy until the tile's items run out instead of each waiting for its own pixel's
 // slowest frames.  Every frame's colour goes to frame_color and hg_blend_frames applies the accumulation blend in
 // frame order afterwards: the same operations in the same order as a lane tracing its pixel's frames in turn.
+__shared__ uint32_t hg_next_item;  // items of the wave's tile handed out so far (one wave per workgroup)
 struct TileItems {
     uint32_t tx0, ty0, tw, nv, n_items, f_begin;  // wave-uniform (scalar registers)
-    uint32_t next_k;                               // items handed out
-    __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe) {
+    __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe, uint32_t lane) {
         const int g = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
         tx0 = uint32_t(g % kp.tiles_x) * HG_TILE;
         ty0 = uint32_t(g / kp.tiles_x) * HG_TILE;
@@ -164,7 +164,8 @@ struct TileItems {
         nv = tw * th;
         n_items = __builtin_amdgcn_readfirstlane(valid && fe > fb ? nv * (fe - fb) : 0u);
         f_begin = fb;
-        next_k = 64u;
+        if (lane == 0) hg_next_item = 64u;  // lane l starts with item l
+        wave_lds_sync();
     }
     // item k -> its pixel within the tile (x + 8 y) and its frame: shifts for a whole tile, divisions at the edge
     __device__ __forceinline__ void get(uint32_t k, uint32_t& pix, uint32_t& frame) const {
@@ -179,12 +180,17 @@ struct TileItems {
         }
         frame = f_begin + q;
     }
-    // every lane calls this (top level): lanes with `need` get the next items in lane order; false: no item is left
-    __device__ __forceinline__ bool take(bool need, uint32_t& pix, uint32_t& frame) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(need);
-        const uint32_t k = next_k + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-        next_k += uint32_t(__builtin_popcountll(m));
-        if (!need || k >= n_items) return false;
+    // Called by exactly the lanes that need an item (the active lanes): they take the next items in lane order.  The
+    // first of them advances the LDS counter with one atomic add and its old value goes to the others by
+    // readfirstlane.  false: the tile's items are all handed out.
+    __device__ __forceinline__ bool take_here(uint32_t& pix, uint32_t& frame) const {
+        const uint64_t m = __builtin_amdgcn_read_exec();
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        uint32_t base = 0;
+        if (rank == 0u) base = atomicAdd(&hg_next_item, uint32_t(__builtin_popcountll(m)));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const uint32_t k = base + rank;
+        if (k >= n_items) return false;
         get(k, pix, frame);
         return true;
     }
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
     Ray ray{mk(0, 0, 0), mk(0, 0, 1)};
     float acc_rough = 0.0f;
 #if HG_REGEN_ITEMS
-    TileItems items(kp, local_tile, chunk < split, f_begin, f_end);
+    const TileItems items(kp, local_tile, chunk < split, f_begin, f_end, lane);
     uint32_t pix = lane;  // the item's pixel within the tile (x + 8 y)
     if (lane < items.n_items) {  // item `lane`
         uint32_t f;
@@ -330,7 +336,6 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
         const uint64_t t0 = kCounters ? wave_clock() : 0;
         const bool was_work = work;
         uint64_t t1 = 0;
-        bool need = false;  // HG_REGEN_ITEMS: this lane's frame is done, it takes the next item
         if (work) {
 #if HG_REGEN_PRIO
             __builtin_amdgcn_s_setprio(1);
@@ -391,14 +396,25 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                         *slot = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    need = HG_REGEN_ITEMS;
-                    if (!HG_REGEN_ITEMS && (fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
+#if HG_REGEN_ITEMS
+                    uint32_t f;
+                    if (items.take_here(pix, f)) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                        next = true;
+                        sum = mk(0, 0, 0);
+                        fs = f << 16;
+                        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u,
+                                      pcg_hash(items.tx0 + (pix & 7u) + (items.ty0 + (pix >> 3)) * kp.Wu), 0u};
+                        ms = MediumStack{0ull, 0};
+                    }
+#else
+                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
                         smp.offset = 0;
                         ms = MediumStack{0ull, 0};
                     }
+#endif
                 }
                 s_sum.set(sum);
                 if (next) {
@@ -411,33 +427,13 @@ __global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(cons
                     acc_rough = 0.0f;
                     bounce = 0;
                     paths++;
-                } else if (!need) {
+                } else {
                     work = false;
                 }
             }
             s_thr.set(thr);
             s_col.set(col);
         }
-#if HG_REGEN_ITEMS
-        if (wave_ballot(need)) {  // lanes whose frame is done take the next items
-            uint32_t f = 0;
-            if (items.take(need, pix, f)) {
-                const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
-                fs = f << 16;
-                smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
-                ms = MediumStack{0ull, 0};
-                ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
-                s_thr.set(mk(1, 1, 1));
-                s_col.set(mk(0, 0, 0));
-                s_sum.set(mk(0, 0, 0));
-                acc_rough = 0.0f;
-                bounce = 0;
-                paths++;
-            } else if (need) {
-                work = false;
-            }
-        }
-#endif
         if (kCounters) {  // t1 was read inside the divergent branch: take it from a lane that ran it
             const uint64_t t2 = wave_clock();
             const int src = __ffsll((unsigned long long)__ballot(was_work)) - 1;
@@ -576,7 +572,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
     Trav tv;
     tv.mi = nm;
 #if HG_STREAM_ITEMS
-    TileItems items(kp, local_tile, chunk < split, f_begin, f_end);
+    const TileItems items(kp, local_tile, chunk < split, f_begin, f_end, lane);
     uint32_t pix = lane;  // the item's pixel within the tile (x + 8 y)
     if (lane < items.n_items) {  // item `lane`
         uint32_t f;
@@ -629,7 +625,6 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
         for (uint32_t it = 0;; ++it) {
             const uint32_t n_sh = wave_count(work && tv.mi >= nm);
             if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
-            bool need = false;  // HG_STREAM_ITEMS: this lane's frame is done, it takes the next item
             if (work && tv.mi >= nm) {
             c.shade_rounds += wave_once();
 #if HG_PHASE_DETAIL == 1
@@ -693,14 +688,25 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                         else kp.acc[slot_i] = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    need = HG_STREAM_ITEMS;
-                    if (!HG_STREAM_ITEMS && (fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
+#if HG_STREAM_ITEMS
+                    uint32_t f;
+                    if (items.take_here(pix, f)) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                        next = true;
+                        sum = mk(0, 0, 0);
+                        fs = f << 16;
+                        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u,
+                                      pcg_hash(items.tx0 + (pix & 7u) + (items.ty0 + (pix >> 3)) * kp.Wu), 0u};
+                        ms = MediumStack{0ull, 0};
+                    }
+#else
+                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
                         next = true;
                         sum = mk(0, 0, 0);
                         smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
                         smp.offset = 0;
                         ms = MediumStack{0ull, 0};
                     }
+#endif
                 }
                 if (!lds_acc) s_sum.set(sum);
                 if (next) {
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
                     bounce = 0;
                     paths++;
                     alive = true;
-                } else if (!need) {
+                } else {
                     work = false;
                 }
             }
@@ -730,27 +736,6 @@ __global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(c
             if (kCounters) tp = phase_mark(kp, 14, tp);
 #endif
             }
-#if HG_STREAM_ITEMS
-            if (wave_ballot(need)) {  // lanes whose frame is done take the next items
-                uint32_t f = 0;
-                if (items.take(need, pix, f)) {
-                    const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
-                    fs = f << 16;
-                    smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(qx + qy * kp.Wu), 0u};
-                    ms = MediumStack{0ull, 0};
-                    ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
-                    s_thr.set(mk(1, 1, 1));
-                    s_col.set(mk(0, 0, 0));
-                    s_sum.set(mk(0, 0, 0));
-                    acc_rough = 0.0f;
-                    bounce = 0;
-                    paths++;
-                    trav_begin<kMeshLds>(kp, ray, tv, c);
-                } else if (need) {
-                    work = false;
-                }
-            }
-#endif
         }
 #if HG_SHADE_PRIO == 1
         __builtin_amdgcn_s_setprio(0);
