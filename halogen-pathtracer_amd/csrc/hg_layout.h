@@ -146,6 +146,9 @@
 #ifndef HG_REGEN_ITEMS
 #define HG_REGEN_ITEMS 1  // regenerating kernel: the same (pixel, frame) item scheduling (HG_STREAM_ITEMS)
 #endif
+#ifndef HG_STREAM_MIN_MESHES
+#define HG_STREAM_MIN_MESHES 4  // HG_KERNEL_AUTO: the streaming kernel from this many meshes on (or for a deep BLAS)
+#endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif

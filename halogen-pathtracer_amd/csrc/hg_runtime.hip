@@ -764,10 +764,14 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (int rc = event_pair(c, ev)) return rc;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
-    // HG_KERNEL_AUTO: the streaming kernel for deep BLAS (its resumable traversal pays off when a few lanes carry
-    // long traversals: C3 +6 %), the regenerating kernel otherwise (C2/C5: stream -18/-20 %) (tools/sweeps/sweep35.txt)
+    // HG_KERNEL_AUTO: the streaming kernel for deep BLAS or many meshes, where traversals are long or uneven and its
+    // resumable traversal lets a lane move on without waiting for the wave's slowest one (C3; C2's 9 meshes: 4,080
+    // vs 3,891 Mpaths/s, tools/sweep_r02_ai.txt); the regenerating kernel for a few shallow meshes, where shading
+    // dominates (C5's 2 meshes: 10,407 vs 9,718).  (Round 1, before the item scheduling and the mesh records in LDS,
+    // the streaming kernel lost C2 too, tools/sweeps/sweep35.txt.)
     const bool deep_blas = c->stack_depth > HG_DESCENT_DEEP + 2;
-    const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (deep_blas ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
+    const bool stream_auto = deep_blas || c->n_meshes >= HG_STREAM_MIN_MESHES;
+    const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (stream_auto ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
                                                      : c->kernel;
     const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     // relaxed descent threshold: 3 for the regen / lockstep kernels, HG_STREAM_DESCENT_T for the streaming one

@@ -223,11 +223,12 @@ def test_gpu_relaxed_descent_bit_exact(gpu, t, kernel):
 
 @pytest.mark.gpu
 def test_gpu_auto_kernel_choice(gpu):
-    """HG_KERNEL_AUTO (the default) runs the streaming kernel for deep BLAS (the 871k dragon) and the regenerating
-    kernel for shallow scenes; the debug views always run the lockstep kernel."""
+    """HG_KERNEL_AUTO (the default) runs the streaming kernel for deep BLAS (the 871k dragon) or scenes of 4 or
+    more meshes (the Cornell box's 9) and the regenerating kernel for a few shallow meshes (the glass scene's 2); the
+    debug views always run the lockstep kernel."""
     with abi.Context(0) as ctx:
         assert ctx.counters()["last_kernel"] == 0
-    for name, want in (("c1_64", abi.HG_KERNEL_MEGA_REGEN), ("glass_64x36", abi.HG_KERNEL_MEGA_REGEN),
+    for name, want in (("c1_64", abi.HG_KERNEL_MEGA_STREAM), ("glass_64x36", abi.HG_KERNEL_MEGA_REGEN),
                        ("c1_32_normal", abi.HG_KERNEL_MEGA)):
         packed, params, cube, frames, acc = cases.setup(name)
         _, cnt = gpu_render(packed, params, frames, acc, cube, kernel="auto")
