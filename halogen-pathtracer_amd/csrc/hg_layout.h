@@ -68,7 +68,8 @@
 #define HG_STREAM_RESHADE 16  // streaming kernel: repeat the shading pass while at least this many lanes need it
 #endif
 #ifndef HG_STREAM_DESCENT_T
-#define HG_STREAM_DESCENT_T 8  // the same for the streaming kernel (tools/sweeps/sweep42.txt; 8 with the unsplit launch, sweep74)
+#define HG_STREAM_DESCENT_T 12  // the same for the streaming kernel (tools/sweeps/sweep42.txt; 8 with the unsplit launch,
+                                // sweep74; 12 with the in-place item scheduling, +2.4 %, tools/sweep_r02_al.txt)
 #endif
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16
