@@ -373,18 +373,6 @@ struct Stack {
     }
     __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const { store(sp++, v); }
     __device__ __forceinline__ uint32_t pop(uint32_t& sp) const { return load(--sp); }
-    // Register-cached top (HG_STACK_TOP): entry sp-1 lives in `top`, entry k < sp-1 in slot k+1 (slot 0 takes the
-    // undefined initial top), so a pop returns at once and the slot read that refills `top` is only waited for
-    // at the next pop.  Same capacity as push/pop.
-    __device__ __forceinline__ void push_c(uint32_t& sp, uint32_t& top, uint32_t v) const {
-        store(sp++, top);
-        top = v;
-    }
-    __device__ __forceinline__ uint32_t pop_c(uint32_t& sp, uint32_t& top) const {
-        const uint32_t v = top;
-        top = load(--sp);
-        return v;
-    }
 };
 using MegaStack = Stack<HG_MEGA_LDS_STACK>;
 
@@ -439,15 +427,6 @@ struct RowStack {
     }
     __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const { store(sp++, v); }
     __device__ __forceinline__ uint32_t pop(uint32_t& sp) const { return load(--sp); }
-    __device__ __forceinline__ void push_c(uint32_t& sp, uint32_t& top, uint32_t v) const {
-        store(sp++, top);
-        top = v;
-    }
-    __device__ __forceinline__ uint32_t pop_c(uint32_t& sp, uint32_t& top) const {
-        const uint32_t v = top;
-        top = load(--sp);
-        return v;
-    }
 };
 
 // first mesh index >= m whose cull bit is set (meshes >= 64 carry no bit and are always live); n if none
@@ -886,9 +865,6 @@ struct Trav {
     uint32_t best_tri;     // triangle | orientation<0 << 31, HG_NONE: no mesh hit yet
     uint32_t best_mesh, sph, node, sp, mi;  // mi == n_meshes: traversal finished
     uint64_t live;         // exact-cull mask of the meshes
-#if HG_STACK_TOP
-    uint32_t top;  // the stack's top entry (Stack::push_c / pop_c)
-#endif
 };
 
 template <bool kMeshLds = false>
@@ -980,15 +956,9 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
             const bool bFirst = dB < dA;  // :430-444
             const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
             const bool nearOk = (bFirst ? dB : dA) < t.best_t, farOk = (bFirst ? dA : dB) < t.best_t;
-#if HG_STACK_TOP
-            if (nearOk && farOk) stk.push_c(t.sp, t.top, farRef);
-            t.node = nearOk ? nearRef : farRef;
-            if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop_c(t.sp, t.top) : HG_NONE;
-#else
             if (nearOk && farOk) stk.push(t.sp, farRef);
             t.node = nearOk ? nearRef : farRef;
             if (!nearOk && !farOk) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
-#endif
         }
         dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     }
@@ -1048,13 +1018,7 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
                 t.best_mesh = t.mi;
             }
         }
-        t.node = t.sp > 0 ?
-#if HG_STACK_TOP
-                 stk.pop_c(t.sp, t.top)
-#else
-                 stk.pop(t.sp)
-#endif
-                 : HG_NONE;
+        t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
     }
 #if HG_PHASE_DETAIL == 3
     if (kp.counters) tp = phase_mark(kp, 12, tp);

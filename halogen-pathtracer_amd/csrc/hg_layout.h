@@ -101,9 +101,6 @@
 #ifndef HG_REGEN_PRIO
 #define HG_REGEN_PRIO 1  // regenerating kernel: wave priority raised during get_ray_intersection (C2 +1 %, C5 +2 %,
 #endif                   // tools/sweeps/sweep69.txt)
-#ifndef HG_STACK_TOP
-#define HG_STACK_TOP 0  // streaming traversal: keep the stack's top entry in a register (pops off the LDS latency)
-#endif
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
