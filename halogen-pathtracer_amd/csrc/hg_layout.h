@@ -147,6 +147,9 @@
 #ifndef HG_STREAM_MIN_MESHES
 #define HG_STREAM_MIN_MESHES 4  // HG_KERNEL_AUTO: the streaming kernel from this many meshes on (or for a deep BLAS)
 #endif
+#ifndef HG_STREAM_LB
+#define HG_STREAM_LB 64  // regen / stream kernels: __launch_bounds__ max threads = their one-wave workgroup (256: scratch 32 B vs 24-28 B)
+#endif
 #ifndef HG_CHECK_EXEC
 #define HG_CHECK_EXEC 0  // debug builds: leaf_dist checks its all-lanes-active precondition (hg_device.h)
 #endif

@@ -273,7 +273,7 @@ hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint
 }
 
 template <bool kCounters, bool kMeshLds>
-__global__ __launch_bounds__(256, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
+__global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     if (kMeshLds) {  // the wave's copy of the mesh records (mesh_f4, hg_device.h)
         mesh_lds_fill(kp, lane);
@@ -521,7 +521,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp_in, int block, bool cou
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
 template <bool kCounters, bool kLdsAcc, bool kMeshLds>
-__global__ __launch_bounds__(256, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
+__global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
     // one wave per workgroup (launched with 64 threads): wave = workgroup
