@@ -1411,12 +1411,25 @@ __device__ __forceinline__ float inv_blackman_harris(float x) {
 
 // get_ray :996-1013 (+ get_ray_jitter :984-994, get_random_point_circle HalogenRandom.hlsl:303-308)
 __device__ Ray camera_ray(const HgKernelParams& kp, const Sampler& smp, float ndcx, float ndcy) {
-    float fd0, fd1, j0, j1;
-    smp.get2(ID_FOCAL, fd0, fd1);
-    const float th = (fd0 * 360.0f) * HG_DEG2RAD;
-    float sth, cth;
-    hg_sincosf(th, &sth, &cth);
-    const f3 ap = mk(cth * kp.focal_disc_radius * fd1, sth * kp.focal_disc_radius * fd1, 0.0f);
+    float j0, j1;
+    f3 ap = mk(0.0f, 0.0f, 0.0f);
+#if HG_PINHOLE_FAST
+    // Pinhole (disc radius 0): ap is (+-0, +-0, 0), the zeros' signs those of cos / sin.  Nothing below can see them
+    // when the camera translation has no zero component (m[3] + (+-0) = m[3] in xform) and pf has no -0 component:
+    // ndcx, ndcy are never -0 (x - 1 rounds an exact 0 to +0), so with vw, vh > 0 screen.x, .y are never -0 either
+    // (+0 + -0 = +0; no sum underflows), and normalize / the focal distance > 0 keep the sign.  Then pf - (+-0) = pf,
+    // and the focal sample and its sincos are skipped: the same bits.
+    if (!(kp.focal_disc_radius == 0.0f && kp.cam[3] != 0.0f && kp.cam[7] != 0.0f && kp.cam[11] != 0.0f &&
+          kp.vw > 0.0f && kp.vh > 0.0f && kp.near_ > 0.0f && kp.focal_dist > 0.0f))
+#endif
+    {
+        float fd0, fd1;
+        smp.get2(ID_FOCAL, fd0, fd1);
+        const float th = (fd0 * 360.0f) * HG_DEG2RAD;
+        float sth, cth;
+        hg_sincosf(th, &sth, &cth);
+        ap = mk(cth * kp.focal_disc_radius * fd1, sth * kp.focal_disc_radius * fd1, 0.0f);
+    }
     f3 screen = mk(ndcx * kp.vw, ndcy * kp.vh, 1.0f * kp.near_);
     smp.get2(ID_JITTER, j0, j1);
     const float jx = (inv_blackman_harris(j0) - 0.5f) * 2.0f * kp.filter_radius * kp.psx;
