@@ -146,6 +146,13 @@ __device__ __forceinline__ void record_tile_cost(uint32_t lane) {
     if (p) atomicAdd(p, (unsigned long long)(wave_clock() - hg_wave_t0[threadIdx.x >> 6]));
 }
 
+// RayColor / SamplesPerPixel (:1060); x / 1 == x exactly (NaN and signed zeros included), so spp 1 skips the divisions
+__device__ __forceinline__ f3 sample_mean(const HgKernelParams& kp, f3 sum) {
+    if (kp.spp == 1) return sum;
+    const float sppf = float(kp.spp);
+    return mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
+}
+
 // (pixel, frame) items of a wave's tile (HG_STREAM_ITEMS / HG_REGEN_ITEMS): with the v pixels of the tile inside the
 // image (a w x h rectangle; all 64 for a whole tile), item k is valid pixel k mod v of frame f_begin + k / v.  Lane l
 // starts with item l; a lane whose frame is done takes the next unassigned item (its rank among the wave's lanes that
@@ -372,12 +379,13 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
             if (!alive) {
-                f3 sum = s_sum.get() + col;  // RayColor += trace_ray(...)
+                // RayColor += trace_ray(...); spp 1: 0 + col == col (col starts at +0 and only has terms added: never -0)
+                const bool one_sample = kp.spp == 1;
+                f3 sum = one_sample ? col : s_sum.get() + col;
                 ++fs;
                 bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
-                    const float sppf = float(kp.spp);
-                    const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
+                    const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
                     if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
                         kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
@@ -416,11 +424,15 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                     }
 #endif
                 }
-                s_sum.set(sum);
+                if (!one_sample) s_sum.set(sum);
                 if (next) {
+#if HG_REGEN_ITEMS
+                    const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
+#else
                     const int gtile = kp.rank + local_tile * kp.n_ranks;
                     const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (pix & 7u);
                     const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (pix >> 3);
+#endif
                     ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     thr = mk(1, 1, 1);
                     col = mk(0, 0, 0);
@@ -664,12 +676,13 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #endif
             if (!alive) {
                 // RayColor += trace_ray(...); with lds_acc (spp 1) the sum is the path's colour (0 + col == col)
-                f3 sum = lds_acc ? col : s_sum.get() + col;
+                // (col is never -0: it starts at +0 and only has terms added, so 0 + col == col bit for bit)
+                const bool one_sample = lds_acc || kp.spp == 1;
+                f3 sum = one_sample ? col : s_sum.get() + col;
                 ++fs;
                 bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
-                    const float sppf = float(kp.spp);
-                    const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
+                    const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
                     if (HG_STREAM_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
                         kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
@@ -708,12 +721,16 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     }
 #endif
                 }
-                if (!lds_acc) s_sum.set(sum);
+                if (!one_sample) s_sum.set(sum);
                 if (next) {
                     {
+#if HG_STREAM_ITEMS
+                        const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
+#else
                         const int gtile = kp.rank + local_tile * kp.n_ranks;
                         const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (pix & 7u);
                         const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (pix >> 3);
+#endif
                         ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     }
                     thr = mk(1, 1, 1);
