@@ -189,17 +189,16 @@ struct TileItems {
     }
     // Called by exactly the lanes that need an item (the active lanes): they take the next items in lane order.  The
     // first of them advances the LDS counter with one atomic add and its old value goes to the others by
-    // readfirstlane.  false: the tile's items are all handed out.
-    __device__ __forceinline__ bool take_here(uint32_t& pix, uint32_t& frame) const {
+    // readfirstlane.  Returns the item's index k, k >= n_items when the tile's items are all handed out; the caller
+    // decodes k with get() inside its branch (decoded here, the frame was held across a control-flow merge and spilled
+    // to scratch at every take).
+    __device__ __forceinline__ uint32_t take_here() const {
         const uint64_t m = __builtin_amdgcn_read_exec();
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
         uint32_t base = 0;
         if (rank == 0u) base = atomicAdd(&hg_next_item, uint32_t(__builtin_popcountll(m)));
         base = __builtin_amdgcn_readfirstlane(base);
-        const uint32_t k = base + rank;
-        if (k >= n_items) return false;
-        get(k, pix, frame);
-        return true;
+        return base + rank;
     }
 };
 
@@ -405,8 +404,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
 #if HG_REGEN_ITEMS
-                    uint32_t f;
-                    if (items.take_here(pix, f)) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                    const uint32_t k = items.take_here();
+                    if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                        uint32_t f;
+                        items.get(k, pix, f);
                         next = true;
                         sum = mk(0, 0, 0);
                         fs = f << 16;
@@ -702,8 +703,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
 #if HG_STREAM_ITEMS
-                    uint32_t f;
-                    if (items.take_here(pix, f)) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                    const uint32_t k = items.take_here();
+                    if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                        uint32_t f;
+                        items.get(k, pix, f);
                         next = true;
                         sum = mk(0, 0, 0);
                         fs = f << 16;
