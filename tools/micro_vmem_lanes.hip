@@ -30,10 +30,11 @@ __global__ __launch_bounds__(64) void loads(const float4* __restrict__ table, ui
 // random record, against only its first 16 B: how much do the extra requests to an already-fetched line cost?
 template <int kLoads>
 __global__ __launch_bounds__(64) void records(const float4* __restrict__ table, uint32_t iters, uint32_t table_f4,
-                                              float* __restrict__ sink) {
+                                              float* __restrict__ sink, uint32_t group) {
     const uint32_t lane = threadIdx.x;
     const uint32_t m = table_f4 / 4u - 1u;  // records of 4 float4
-    uint32_t r = (blockIdx.x * 977u + lane * 131u) & m;
+    // `group` consecutive lanes share a record (1: every lane its own line; 64: the whole wave on one record)
+    uint32_t r = (blockIdx.x * 977u + (lane / group) * 131u) & m;
     float acc = 0.0f;
     for (uint32_t i = 0; i < iters; ++i) {
         const float4* p = table + 4u * r;
@@ -75,21 +76,25 @@ int main() {
         printf("{\"active_lanes\": %u, \"ms\": %.3f, \"wave_loads_per_ns\": %.3f, \"lane_loads_per_ns\": %.3f}\n", n, best,
                insts / (best * 1e6), insts * n / (best * 1e6));
     }
-    for (int k : {1, 4}) {
-        float best = 1e30f;
-        for (int rep = 0; rep < 3; ++rep) {
-            (void)hipEventRecord(a);
-            if (k == 1) hipLaunchKernelGGL(records<1>, dim3(blocks), dim3(64), 0, 0, table, iters, table_f4, sink);
-            else hipLaunchKernelGGL(records<4>, dim3(blocks), dim3(64), 0, 0, table, iters, table_f4, sink);
-            (void)hipEventRecord(b);
-            (void)hipEventSynchronize(b);
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, a, b);
-            if (ms < best) best = ms;
+    for (uint32_t group : {1u, 8u, 64u}) {
+        for (int k : {1, 4}) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 3; ++rep) {
+                (void)hipEventRecord(a);
+                if (k == 1)
+                    hipLaunchKernelGGL(records<1>, dim3(blocks), dim3(64), 0, 0, table, iters, table_f4, sink, group);
+                else
+                    hipLaunchKernelGGL(records<4>, dim3(blocks), dim3(64), 0, 0, table, iters, table_f4, sink, group);
+                (void)hipEventRecord(b);
+                (void)hipEventSynchronize(b);
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, a, b);
+                if (ms < best) best = ms;
+            }
+            const double recs = double(blocks) * iters * 64;
+            printf("{\"lanes_per_record\": %u, \"record_loads_per_lane_step\": %d, \"ms\": %.3f, "
+                   "\"lane_steps_per_ns\": %.3f}\n", group, k, best, recs / (best * 1e6));
         }
-        const double recs = double(blocks) * iters * 64;
-        printf("{\"record_loads_per_lane_step\": %d, \"ms\": %.3f, \"lane_steps_per_ns\": %.3f}\n", k, best,
-               recs / (best * 1e6));
     }
     (void)hipFree(table);
     (void)hipFree(sink);
