@@ -102,7 +102,8 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
     build, over the launch time measured live with HIP events) against 1,024 SIMDs x 2.4 GHz / 2 cycles.
     lane_util is the mean fraction of the 64 lanes active in those instructions, so frac x lane_util is the share of
     the chip's fp32 lane-issue slots doing work.  HBM stays beside it: the PMC-measured DRAM-side bytes (traffic)
-    against 8 TB/s, and the §8(d) logical bytes."""
+    against 8 TB/s, and the §8(d) logical bytes.  vmem_unit_busy is the busy share of the vector-memory data path
+    (TD) from the same committed profile: the unit that binds the traversal, beside the VALU figure."""
     ok = mean_launch_s > 0
     valu = pmc.get("valu_insts_per_launch")
     achieved = valu / mean_launch_s / 1e9 if valu and ok else None
@@ -114,6 +115,8 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "unit_note": "wave64 VALU instructions issued per second (peak = 1024 SIMDs x 2.4 GHz / 2 cycles)",
             "frac": frac, "lane_util": lane, "useful_lane_frac": frac * lane if frac and lane else None,
             "wait_any_frac": pmc.get("wait_any_frac"), "l2_hit_rate": pmc.get("l2_hit_rate"),
+            # the unit that binds: the texture-data path's busy share of the launch (PMC TD_TD_BUSY)
+            "vmem_unit_busy": pmc.get("vmem_unit_busy"),
             "traffic": traffic,
             "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and ok else None,
             "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS if traffic and ok else None,

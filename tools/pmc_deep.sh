@@ -1,7 +1,7 @@
 #!/bin/bash
 # Memory-pipeline counters of the timed trace kernel (TA/TD/TCP/SQ levels), one rocprofv3 --pmc pass per group,
-# each under its own time limit; any failure ends the script.  Output: gpurun_out/prof/<TAG>_deep<k>/.
-#   TAG=r02d bash tools/pmc_deep.sh ; python tools/pmc_table.py gpurun_out/prof/r02d_deep*
+# each under its own time limit; any failure ends the script.  Output: gpurun_out/prof/deep<k>_<TAG>/ (outside the summarizer's <TAG>_* glob).
+#   TAG=r02d bash tools/pmc_deep.sh ; python tools/pmc_table.py gpurun_out/prof/deep*_r02d
 set -u
 TAG=${TAG:-deep}
 ARGS=${BENCH_ARGS:---steps 4 --warmup 1 --no-cpu-baseline --no-framed}
@@ -12,9 +12,9 @@ k=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   k=$((k + 1))
-  timeout -s KILL 120 rocprofv3 --pmc $counters -d "$OUT/${TAG}_deep$k" -o deep --output-format csv -- \
-      python3 bench.py $ARGS > "$OUT/${TAG}_deep$k.log" 2>&1
-  rc=$?; echo "pass $k rc=$rc ($counters)"; [ $rc -eq 0 ] || { tail -5 "$OUT/${TAG}_deep$k.log"; exit $rc; }
+  timeout -s KILL 120 rocprofv3 --pmc $counters -d "$OUT/deep${k}_${TAG}" -o deep --output-format csv -- \
+      python3 bench.py $ARGS > "$OUT/deep${k}_${TAG}.log" 2>&1
+  rc=$?; echo "pass $k rc=$rc ($counters)"; [ $rc -eq 0 ] || { tail -5 "$OUT/deep${k}_${TAG}.log"; exit $rc; }
 done <<'LIST'
 TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE
 TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum

@@ -18,4 +18,5 @@ run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run valu --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 run mem --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY TCC_HIT_sum TCC_MISS_sum
+run td --pmc TA_BUSY_avr TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE
 find "$OUT" -name "*.csv" | head -50

@@ -24,6 +24,7 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
+N_CU, N_XCD = 256, 8  # MI355X
 
 
 def kname(raw: str) -> str:
@@ -87,6 +88,12 @@ def main():
             wc = pmc["SQ_WAVE_CYCLES"]
             d["wave_cycle_split"] = {"wait_any": pmc.get("SQ_WAIT_ANY", 0) / wc,
                                      "wait_inst_any": pmc.get("SQ_WAIT_INST_ANY", 0) / wc}
+        if "TD_TD_BUSY_sum" in pmc and pmc.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; the TD/TA counters sum (or average) over the 256 CUs (MI355X)
+            cyc = pmc["GRBM_GUI_ACTIVE"] / N_XCD
+            d["vmem_unit_busy"] = {"td_busy": pmc["TD_TD_BUSY_sum"] / (N_CU * cyc),
+                                   "td_stalled_on_l1": pmc.get("TD_TC_STALL_sum", 0) / (N_CU * cyc),
+                                   "ta_busy": pmc.get("TA_BUSY_avr", 0) / cyc}
         kernels[k] = d
     summary = {"tag": a.tag, "command": f"rocprofv3 --kernel-trace --stats | --pmc <group> -- {a.command}",
                "config": a.config, "width": a.width, "height": a.height,
@@ -115,6 +122,8 @@ def main():
             t["wait_any_frac"] = k["wave_cycle_split"].get("wait_any")
         if "l2_hit_rate" in k:
             t["l2_hit_rate"] = k["l2_hit_rate"]
+        if "vmem_unit_busy" in k:
+            t["vmem_unit_busy"] = k["vmem_unit_busy"]
         (out / "pmc_traffic.json").write_text(json.dumps(t, indent=1) + "\n")
     print(json.dumps(summary, indent=1))
 
