@@ -92,6 +92,9 @@
 #ifndef HG_LEAF_DIST
 #define HG_LEAF_DIST 1  // streaming traversal: a round's (ray, triangle) pairs dealt over all 64 lanes, LDS min-reduce
 #endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweeps/sweep52.txt)
+#ifndef HG_ORDER_BUCKETS
+#define HG_ORDER_BUCKETS 1024  // hg_order_tiles: cost buckets of the longest-first order (tile-index order within one)
+#endif
 #ifndef HG_PINHOLE_FAST
 #define HG_PINHOLE_FAST 1  // camera_ray skips the focal-disc sample when the disc radius is 0 (same bits, hg_device.h)
 #endif

@@ -224,10 +224,13 @@ __global__ __launch_bounds__(1024) void hg_order_tiles(unsigned long long* __res
     atomicMax(&cmax, m);
     __syncthreads();
     const unsigned long long top = cmax;
-    // bucket = 1023 - floor(c * 1024 / (top + 1)), in 128-bit-safe form (c <= top)
+    // bucket = B-1 - floor(c * B / (top + 1)) for B = HG_ORDER_BUCKETS <= 1024, in 128-bit-safe form (c <= top);
+    // within a bucket the tiles keep their index order
     auto bucket = [top](unsigned long long c) -> uint32_t {
-        const unsigned long long q = top / 1024u + 1u;  // c / q < 1024 for every c <= top
-        return 1023u - uint32_t(c / q);
+        constexpr uint32_t B = HG_ORDER_BUCKETS;
+        static_assert(B >= 1 && B <= 1024, "order buckets");
+        const unsigned long long q = top / B + 1u;  // c / q < B for every c <= top
+        return B - 1u - uint32_t(c / q);
     };
     for (uint32_t i = t; i < n; i += 1024) atomicAdd(&start[bucket(cost[i])], 1u);
     __syncthreads();
