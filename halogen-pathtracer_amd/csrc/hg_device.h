@@ -220,6 +220,15 @@ __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
+// Frame colour of launch frame f (0 .. n_frames-1) for accumulator slot `slot` (hg_blend_frames reads the same layout)
+__device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f, size_t slot) {
+#if HG_FC_SLOT_MAJOR
+    return slot * size_t(uint32_t(kp.n_frames)) + f;
+#else
+    return size_t(f) * (size_t(uint32_t(kp.n_local_tiles)) * 64u) + slot;
+#endif
+}
+
 // Triangle ti's Moller-Trumbore operands from the three SoA streams: a = (v0, e1.x), b = (e1.yz, e2.xy), cz = e2.z.
 // (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md.)
 __device__ __forceinline__ void tri_load(const HgKernelParams& kp, uint32_t ti, float4& a, float4& b, float& cz) {

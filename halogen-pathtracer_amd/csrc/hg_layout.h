@@ -147,6 +147,13 @@
 #ifndef HG_STREAM_ITEMS
 #define HG_STREAM_ITEMS 1  // streaming kernel: lanes take (pixel, frame) items of the wave's tile (frame colours blended after)
 #endif
+#ifndef HG_FC_SLOT_MAJOR
+#define HG_FC_SLOT_MAJOR 1  // frame colours stored [slot][frame] (a pixel's frames contiguous) instead of [frame][slot]
+#endif
+#ifndef HG_ITEMS_PIXEL_MAJOR
+#define HG_ITEMS_PIXEL_MAJOR 1  // items k -> (pixel k / frames, frame k % frames): a wave's lanes trace one pixel's frames
+                                // (with HG_FC_SLOT_MAJOR: C3 +0.4 %, C2 +0.5 %, C5 -0.4 %; tools/sweeps/sweep_r02_be/bf)
+#endif
 #ifndef HG_REGEN_ITEMS
 #define HG_REGEN_ITEMS 1  // regenerating kernel: the same (pixel, frame) item scheduling (HG_STREAM_ITEMS)
 #endif
@@ -197,7 +204,7 @@ struct HgKernelParams {
     int32_t n_spheres, n_meshes;
     int32_t first_frame, n_frames, accumulate;
     // frame-parallel split (regenerating kernel): frame_split waves share each tile, wave k tracing frames
-    // [k*n_frames/split, (k+1)*n_frames/split) into frame_color[frame][slot]; hg_blend_frames then applies the
+    // [k*n_frames/split, (k+1)*n_frames/split) into frame_color (fc_index); hg_blend_frames then applies the
     // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
     int32_t frame_split;
     float4* __restrict__ frame_color;

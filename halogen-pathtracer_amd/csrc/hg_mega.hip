@@ -162,6 +162,9 @@ __device__ __forceinline__ f3 sample_mean(const HgKernelParams& kp, f3 sum) {
 __shared__ uint32_t hg_next_item;  // items of the wave's tile handed out so far (one wave per workgroup)
 struct TileItems {
     uint32_t tx0, ty0, tw, nv, n_items, f_begin;  // wave-uniform (scalar registers)
+#if HG_ITEMS_PIXEL_MAJOR
+    uint32_t nf;  // frames of the chunk
+#endif
     __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe, uint32_t lane) {
         const int g = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
         tx0 = uint32_t(g % kp.tiles_x) * HG_TILE;
@@ -171,12 +174,29 @@ struct TileItems {
         nv = tw * th;
         n_items = __builtin_amdgcn_readfirstlane(valid && fe > fb ? nv * (fe - fb) : 0u);
         f_begin = fb;
+#if HG_ITEMS_PIXEL_MAJOR
+        nf = __builtin_amdgcn_readfirstlane(fe > fb ? fe - fb : 1u);
+#endif
         if (lane == 0) hg_next_item = 64u;  // lane l starts with item l
         wave_lds_sync();
     }
     // item k -> its pixel within the tile (x + 8 y) and its frame: shifts for a whole tile, divisions at the edge
     __device__ __forceinline__ void get(uint32_t k, uint32_t& pix, uint32_t& frame) const {
         uint32_t q;
+#if HG_ITEMS_PIXEL_MAJOR  // item k -> valid pixel k / nf, frame k mod nf (a wave's lanes on one pixel's frames)
+        uint32_t i;
+        if ((nf & (nf - 1u)) == 0u) {
+            const uint32_t lg = uint32_t(__builtin_ctz(nf));
+            i = k >> lg;
+            q = k & (nf - 1u);
+        } else {
+            i = k / nf;
+            q = k - i * nf;
+        }
+        pix = nv == 64u ? i : (i % tw) + 8u * (i / tw);
+        frame = f_begin + q;
+        return;
+#endif
         if (nv == 64u) {
             pix = k & 63u;
             q = k >> 6;
@@ -390,7 +410,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
                     if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
-                        kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
+                        kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
                         float4* slot = kp.acc + slot_i;
@@ -487,7 +507,11 @@ __global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc,
     if (i >= n_slots) return;
     float4 a = acc[i];
     for (int32_t f = 0; f < n_frames; ++f) {
+#if HG_FC_SLOT_MAJOR
+        const float4 c = colors[size_t(i) * uint32_t(n_frames) + uint32_t(f)];  // fc_index (hg_device.h)
+#else
         const float4 c = colors[size_t(f) * n_slots + i];
+#endif
         if (accumulate) {
             const float w = rcp_exact(float(uint32_t(first_frame + f)));
             const float k = 1.0f - w;
@@ -499,11 +523,55 @@ __global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc,
     acc[i] = a;
 }
 
+#if HG_FC_SLOT_MAJOR
+// The same blend over the [slot][frame] layout: each wave owns 64 slots (a tile) and moves their colours 8 frames at
+// a time through LDS, so every load instruction reads whole 128-B lines (8 lanes per line: one slot's 8 frames)
+// instead of 64 lanes on 64 lines; then each lane blends its slot's 8 frames in frame order.
+__global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ acc, const float4* __restrict__ colors,
+                                                          uint32_t n_slots, int32_t n_frames, int32_t first_frame,
+                                                          int32_t accumulate) {
+    constexpr uint32_t kRow = 9;  // float4 per slot row: 8 frames + 1 pad (spreads the lanes' rows over the banks)
+    __shared__ float4 stage[4][64 * kRow];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t slot0 = (blockIdx.x * 4u + w) * 64u;
+    if (slot0 >= n_slots) return;  // whole wave: n_slots is a multiple of 64
+    const uint32_t nf = uint32_t(n_frames);
+    float4* st = stage[w];
+    float4 a = acc[slot0 + lane];
+    for (uint32_t f0 = 0; f0 < nf; f0 += 8u) {
+#pragma unroll
+        for (uint32_t r = 0; r < 8u; ++r) {
+            const uint32_t j = lane + 64u * r, s = j >> 3, ff = j & 7u;
+            if (f0 + ff < nf) st[s * kRow + ff] = colors[size_t(slot0 + s) * nf + f0 + ff];
+        }
+        wave_lds_sync();
+        const uint32_t fe = nf - f0 < 8u ? nf - f0 : 8u;
+        for (uint32_t ff = 0; ff < fe; ++ff) {
+            const float4 c = st[lane * kRow + ff];
+            if (accumulate) {
+                const float wt = rcp_exact(float(uint32_t(first_frame) + f0 + ff));
+                const float k = 1.0f - wt;
+                a = make_float4(a.x * k + c.x * wt, a.y * k + c.y * wt, a.z * k + c.z * wt, a.w * k + 1.0f * wt);
+            } else {
+                a = make_float4(c.x, c.y, c.z, 1.0f);
+            }
+        }
+        wave_lds_sync();
+    }
+    acc[slot0 + lane] = a;
+}
+#endif
+
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) {
     const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
     if (n_slots == 0) return hipSuccess;
+#if HG_FC_SLOT_MAJOR
+    hipLaunchKernelGGL(hg_blend_frames_sm, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc,
+                       kp.frame_color, n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+#else
     hipLaunchKernelGGL(hg_blend_frames, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc, kp.frame_color,
                        n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+#endif
     return hipGetLastError();
 }
 
@@ -689,7 +757,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
                     if (HG_STREAM_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
-                        kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + slot_i] =
+                        kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
                         float4 acc = lds_acc ? s_acc.get() : kp.acc[slot_i];

@@ -295,7 +295,7 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                         const float sppf = float(kp.spp);
                         const f3 color = mk(sum.x / sppf, sum.y / sppf, sum.z / sppf);
                         if (split > 1u) {  // frame-parallel: this frame's colour, blended later in frame order
-                            kp.frame_color[size_t(fs >> 16) * (size_t(nlt) * 64u) + q.slot_i] =
+                            kp.frame_color[fc_index(kp, fs >> 16, q.slot_i)] =
                                 make_float4(color.x, color.y, color.z, 1.0f);
                         } else {
                             float4* slot = kp.acc + q.slot_i;
