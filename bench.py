@@ -89,6 +89,52 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
             "tri_tests_per_path": c["tri_tests"] / c["paths"], "camera_position": list(scenes.CORNELL_FRAMED_CAMERA_POS)}
 
 
+def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_value: float) -> dict:
+    """The drop-in's operating point: the reference dispatches HalogenCompute once per frame (RP:327, RP:406) and the
+    C# shim does hg_render(ctx, 1, 1) per Execute.  The same C3 step (`frames` progressive frames from a cleared
+    accumulator) is rendered as `frames` x hg_render(1) and compared bit for bit with one hg_render(frames); then timed
+    without a host copy (`reps` steps; device sync on both sides) and with the per-frame hg_readback of the 33 MB
+    image the C# pass does (HalogenRenderPass.cs Execute)."""
+    def fresh():
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+
+    fresh()
+    ctx.render(frames, True)
+    batched = ctx.readback(W, H)
+    fresh()
+    for _ in range(frames):
+        ctx.render(1, True)
+    single = ctx.readback(W, H)
+    identical = bool(np.array_equal(batched.view(np.uint32), single.view(np.uint32)))
+    ctx.reset_counters()
+    fresh()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for _ in range(frames):
+            ctx.render(1, True)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    c = ctx.counters()
+    img = np.empty((H, W, 4), np.float32)
+    fresh()
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(frames):
+        ctx.render(1, True)
+        ctx.readback(W, H, img)
+    dt_rb = time.perf_counter() - t1
+    paths = W * H * frames
+    value = paths * reps / dt / 1e6
+    return {"workload": f"{frames} x hg_render(1) per step (RP:327 one dispatch per frame)", "value": value,
+            "unit": "Mpaths/s", "steps": reps, "ms_per_frame": dt * 1e3 / (reps * frames),
+            "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1), "frac_of_batched": value / batched_value,
+            "with_readback": {"value": paths / dt_rb / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_rb * 1e3 / frames,
+                              "readback_bytes_per_frame": W * H * 16},
+            "bit_identical_to_batched": identical}
+
+
 def library_sha256() -> str:
     import hashlib
 
@@ -168,6 +214,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-framed", action="store_true", help="skip the C3F (box opening fills the frame) measurement")
+    ap.add_argument("--no-per-frame", action="store_true", help="skip the one-dispatch-per-frame leg")
+    ap.add_argument("--per-frame-only", action="store_true",
+                    help="profiling aid: only the per-frame leg's timed part (no headline line)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
@@ -178,10 +227,13 @@ def main():
     ap.add_argument("--save-image", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
-    ap.add_argument("--gather", default="", choices=["", "abi", "torch"],
-                    help="N > 1: the final tile gather through the C-ABI (hg_comm, RCCL; default with --dist-backend "
-                         "nccl) or through torch.distributed (default with gloo: the one-GPU rehearsal, where RCCL "
-                         "refuses two ranks on one device)")
+    ap.add_argument("--gather", default="torch", choices=["abi", "torch"],
+                    help="N > 1: the timed tile gather through torch.distributed (default: all_gather_into_tensor, then "
+                         "the C-ABI's host assembly) or through the C-ABI (hg_comm, RCCL send/recv + device assembly)")
+    ap.add_argument("--no-abi-check", action="store_true",
+                    help="N > 1 with nccl and the torch gather: skip the untimed hg_comm (RCCL) gather that is compared "
+                         "bit for bit with the timed gather (its failures are reported in the line, never hang: "
+                         "every hg_comm wait has a deadline)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
@@ -247,14 +299,35 @@ def main():
     ctx.set_tiling(rank, emu or world)
     ctx.set_params(params)
     comm = None
-    gather_mode = args.gather or ("abi" if args.dist_backend == "nccl" else "torch")
-    if dist is not None and gather_mode == "abi":  # hg_comm over RCCL: rank 0 makes the id, every rank joins
+    gather_mode = args.gather
+
+    def join_comm():  # hg_comm over RCCL: rank 0 makes the id, every rank joins (bounded by the comm deadline)
         box = [abi.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        comm = abi.Comm.rank(ctx, world, box[0], rank)
+        return abi.Comm.rank(ctx, world, box[0], rank)
+
+    if dist is not None and gather_mode == "abi":
+        comm = join_comm()
     setup_s = time.perf_counter() - t_setup
 
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
+    if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step, then steps x frames x hg_render(1)
+        ctx.render(frames_per_step, True)
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+        ctx.reset_counters()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps * frames_per_step):
+            ctx.render(1, True)
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        c = ctx.counters()
+        print(json.dumps({"per_frame_only": True, "value": W * H * frames_per_step * args.steps / dt / 1e6,
+                          "unit": "Mpaths/s", "launches": c["launches"],
+                          "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1)}), flush=True)
+        ctx.close()
+        return
     for _ in range(args.warmup):
         ctx.render(frames_per_step, True)
     ctx.synchronize()
@@ -277,7 +350,8 @@ def main():
         ctx.render(frames_per_step, True)
     gathered = None
     if comm is not None:
-        comm.gather(0)  # enqueued on the context stream after the renders; the barrier below waits for it
+        comm.gather(0)  # enqueued on the context stream after the renders
+        comm.synchronize()  # bounded wait (deadline + RCCL async errors) before the barrier's unbounded one
     elif dist is not None:
         import torch
 
@@ -291,6 +365,22 @@ def main():
     dt = time.perf_counter() - t0
     if comm is not None and rank == 0:
         gathered = comm.readback(W, H)
+
+    abi_check = None
+    if dist is not None and comm is None and args.dist_backend == "nccl" and not args.no_abi_check:
+        # untimed: the C-ABI gather (RCCL send/recv + device assembly) of the same accumulators, bit for bit against the
+        # timed torch gather.  hg_comm waits are bounded, so a failure is reported here instead of hanging the ranks.
+        try:
+            with join_comm() as c2:
+                c2.gather(0)
+                c2.synchronize()
+                same = None
+                if rank == 0:
+                    img2 = c2.readback(W, H)
+                    same = bool(np.array_equal(img2.view(np.uint32), np.asarray(gathered).view(np.uint32)))
+                abi_check = {"ok": True, "transport": c2.transport, "bit_identical_to_timed_gather": same}
+        except abi.HalogenError as e:
+            abi_check = {"ok": False, "error": str(e)[:400]}
 
     timing = ctx.counters()  # kernel_ms / launches of the timed launches
     kernel_symbol = KERNEL_SYMBOL.get(int(timing["last_kernel"]), "?")  # the variant HG_KERNEL_AUTO resolved to
@@ -386,8 +476,10 @@ def main():
             "emulated_ranks": emu or None,
             # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
             "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,
-            "gather": (gather_mode + (f" (hg_comm transport {comm.transport})" if comm is not None else ""))
+            "gather": (gather_mode + (f" (hg_comm transport {comm.transport})" if comm is not None else
+                                      " (all_gather_into_tensor + hg_comm_assemble_host)"))
             if dist is not None else None,
+            "abi_gather_check": abi_check,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},
@@ -397,6 +489,9 @@ def main():
             img = (gathered if isinstance(gathered, np.ndarray) else gathered.cpu().numpy()) if gathered is not None \
                 else timed_img
             np.save(args.save_image, img)
+        if world == 1 and not emu and not args.no_per_frame:
+            result["per_frame"] = per_frame_measurement(ctx, params, W, H, frames_per_step, max(2, args.steps // 4),
+                                                        result["value"])
         if world == 1 and not emu and args.config == "C3" and not args.no_counters and not args.no_framed:
             result["framed"] = framed_measurement(ctx, packed, s, W, H, frames_per_step, max(2, args.steps // 4))
         if world == 1 and not args.no_cpu_baseline:

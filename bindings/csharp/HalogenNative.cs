@@ -60,6 +60,7 @@ public static class HalogenNative
         [MarshalAs(UnmanagedType.ByValArray, SizeConst = 4)] public ulong[] shade_detail;
         public ulong shade_rounds;
         public ulong primary_misses;
+        public ulong exec_fallbacks;
     }
 
     public const int HG_OK = 0;
@@ -67,7 +68,7 @@ public static class HalogenNative
                      HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8;
-    public const int HG_SELFTEST_RCP = 1;
+    public const int HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2, HG_BUILD_CHECK_EXEC = 1;
     public const int HG_COMM_ID_BYTES = 128, HG_COMM_RCCL = 1, HG_COMM_PEER = 2;
 
     [DllImport(Lib)] public static extern int hg_abi_version();
@@ -87,6 +88,7 @@ public static class HalogenNative
     [DllImport(Lib)] public static extern int hg_render(IntPtr ctx, int nFrames, int accumulate);
     [DllImport(Lib)] public static extern int hg_synchronize(IntPtr ctx);
     [DllImport(Lib)] public static extern int hg_readback(IntPtr ctx, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_set_accumulation(IntPtr ctx, float[] rgba, UIntPtr nFloats, int frameCount);
     [DllImport(Lib)] public static extern int hg_copy_tiles_device(IntPtr ctx, IntPtr dstDevice, UIntPtr nBytes);
     [DllImport(Lib)] public static extern int hg_local_tile_count(IntPtr ctx);
     [DllImport(Lib)] public static extern int hg_get_counters(IntPtr ctx, out HgCounters c);
@@ -110,10 +112,14 @@ public static class HalogenNative
         out IntPtr comm);
     [DllImport(Lib)] public static extern int hg_comm_init_all(IntPtr[] ctxs, int nRanks, out IntPtr comm);
     [DllImport(Lib)] public static extern int hg_comm_gather(IntPtr comm, int root);
+    [DllImport(Lib)] public static extern int hg_comm_synchronize(IntPtr comm);
     [DllImport(Lib)] public static extern int hg_comm_readback(IntPtr comm, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_comm_set_timeout_ms(IntPtr comm, long timeoutMs);
     [DllImport(Lib)] public static extern int hg_comm_transport(IntPtr comm);
     [DllImport(Lib)] public static extern IntPtr hg_comm_last_error(IntPtr comm);
     [DllImport(Lib)] public static extern void hg_comm_destroy(IntPtr comm);
+    [DllImport(Lib)] public static extern int hg_comm_assemble_host(float[] slabs, long slabTiles, int width,
+        int height, int nRanks, [Out] float[] rgba, UIntPtr nFloats);
 
     public static void Check(IntPtr ctx, int rc, string what)
     {

@@ -13,29 +13,53 @@
 // hg_comm_init_all over contexts that share a device (a one-GPU rehearsal; RCCL refuses two ranks on one GPU) moves
 // the slabs with device copies ordered by events instead.  Either way every byte the root reads was produced by a
 // kernel or copy on a stream the root's stream waits on: no host-visible buffer, no foreign stream.
+//
+// Failure behaviour (SURVEY.md §5 "failure detection"): nothing here waits without a deadline.
+//   - hg_comm_init_rank builds a NON-BLOCKING communicator and polls ncclCommGetAsyncError until it is ready;
+//   - every gather first agrees on the target size and tiling of all ranks (one 5-int ncclAllReduce, max of (v, -v)),
+//     so a mismatched rank fails the gather on EVERY rank with the same text instead of leaving its peers blocked in
+//     mismatched sends / receives; every ncclGroupStart is closed by its ncclGroupEnd on every path;
+//   - waits (the agreement, hg_comm_synchronize, hg_comm_readback) poll the member streams and
+//     ncclCommGetAsyncError; the deadline (hg_comm_set_timeout_ms, env HALOGEN_COMM_TIMEOUT_MS, default 120 s) starts
+//     once this process's own renders ahead of the gather have retired, so only a missing or failed peer trips it.
+//     On an RCCL error or a missed deadline every member communicator is aborted (ncclCommAbort) and the call returns
+//     HG_E_COMM with text; the comm stays unusable (HG_E_COMM) until destroyed.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "halogen_abi.h"
 #include "hg_ctx.h"
 #include "hg_layout.h"
+#include "hg_tiling.h"
+
+namespace {
+constexpr int kAgreeInts = 5;  // W, H, -W, -H, bad tiling (max-reduced: equal on every rank iff max == -max(-v))
+}
 
 struct hg_comm {
     int32_t n_ranks = 0;
     int32_t transport = HG_COMM_RCCL;
+    int64_t timeout_ms = 120000;
+    bool aborted = false;
     std::string err;
     struct Member {
         hg_ctx* ctx = nullptr;
         int32_t rank = 0;
         ncclComm_t nccl = nullptr;  // RCCL transport
         hipEvent_t done = nullptr;  // peer transport: this rank's slab copy is complete (root: slabs free to write)
+        hipEvent_t ready = nullptr;  // RCCL transport: recorded before this member's RCCL work (starts the deadline)
+        int32_t* agree_dev = nullptr;   // RCCL transport: the agreement vector on the member's device
+        int32_t* agree_host = nullptr;  // pinned: [0, 5) sent, [5, 10) received
     };
     std::vector<Member> members;  // the ranks driven by this process
     // root side (the member that last acted as root): staging slabs and the assembled image
@@ -62,14 +86,106 @@ int cfail(hg_comm* m, int code, const char* fmt, ...) {
         hipError_t e_ = (call);                                                                              \
         if (e_ != hipSuccess) return cfail((comm), HG_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
     } while (0)
-#define HG_CNCCL(comm, call)                                                                                     \
-    do {                                                                                                         \
-        ncclResult_t r_ = (call);                                                                                \
-        if (r_ != ncclSuccess) return cfail((comm), HG_E_COMM, "%s failed: %s", #call, ncclGetErrorString(r_)); \
-    } while (0)
 
-int64_t local_tiles(int64_t total, int32_t rank, int32_t n) {
-    return total > rank ? (total - rank + n - 1) / n : 0;
+int64_t env_timeout_ms() {
+    const char* v = std::getenv("HALOGEN_COMM_TIMEOUT_MS");
+    if (!v || !*v) return 120000;
+    const long long t = std::atoll(v);
+    return t > 0 ? int64_t(t) : 120000;
+}
+
+using Clock = std::chrono::steady_clock;
+
+// Abort every member communicator (RCCL's kernels of an aborted comm return) and make the comm unusable.
+void abort_all(hg_comm* m) {
+    for (auto& mb : m->members)
+        if (mb.nccl) {
+            (void)ncclCommAbort(mb.nccl);
+            mb.nccl = nullptr;
+        }
+    m->aborted = true;
+}
+
+// An RCCL error on any member communicator (remote failures surface here), or ncclSuccess / ncclInProgress
+ncclResult_t async_state(hg_comm* m, int32_t* bad_rank) {
+    ncclResult_t worst = ncclSuccess;
+    for (auto& mb : m->members) {
+        if (!mb.nccl) continue;
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(mb.nccl, &st);
+        if (r != ncclSuccess) st = r;
+        if (st != ncclSuccess && st != ncclInProgress) {
+            *bad_rank = mb.rank;
+            return st;
+        }
+        if (st == ncclInProgress) worst = ncclInProgress;
+    }
+    return worst;
+}
+
+// Wait until every member communicator has finished its pending (non-blocking) operation: init, or a group call.
+int wait_comms_ready(hg_comm* m, const char* what) {
+    const auto deadline = Clock::now() + std::chrono::milliseconds(m->timeout_ms);
+    for (;;) {
+        int32_t bad = -1;
+        const ncclResult_t st = async_state(m, &bad);
+        if (st == ncclSuccess) return HG_OK;
+        if (st != ncclInProgress) {
+            abort_all(m);
+            return cfail(m, HG_E_COMM, "%s: RCCL error on rank %d: %s (communicator aborted)", what, bad,
+                         ncclGetErrorString(st));
+        }
+        if (Clock::now() > deadline) {
+            abort_all(m);
+            return cfail(m, HG_E_COMM, "%s: not complete after %lld ms (a peer rank missing or stalled?); "
+                                       "communicator aborted", what, (long long)m->timeout_ms);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// Wait for every member stream to drain.  The deadline starts once each member's `ready` event (recorded ahead of its
+// RCCL work) has completed, i.e. once this process's own renders are done; RCCL errors are polled throughout.
+int wait_streams(hg_comm* m, const char* what) {
+    bool armed = m->transport != HG_COMM_RCCL;  // the peer transport has no remote party: plain deadline
+    auto deadline = Clock::now() + std::chrono::milliseconds(m->timeout_ms);
+    for (;;) {
+        bool all_done = true, all_ready = true;
+        for (auto& mb : m->members) {
+            HG_CHIP(m, hipSetDevice(mb.ctx->device));
+            const hipError_t e = hipStreamQuery(mb.ctx->stream);
+            if (e == hipErrorNotReady) {
+                all_done = false;
+            } else if (e != hipSuccess) {
+                return cfail(m, HG_E_HIP, "%s: stream of rank %d: %s", what, mb.rank, hipGetErrorString(e));
+            }
+            if (!armed && mb.ready) {
+                const hipError_t r = hipEventQuery(mb.ready);
+                if (r == hipErrorNotReady) all_ready = false;
+                else if (r != hipSuccess)
+                    return cfail(m, HG_E_HIP, "%s: event of rank %d: %s", what, mb.rank, hipGetErrorString(r));
+            }
+        }
+        if (all_done) return HG_OK;
+        if (!armed && all_ready) {
+            armed = true;
+            deadline = Clock::now() + std::chrono::milliseconds(m->timeout_ms);
+        }
+        int32_t bad = -1;
+        const ncclResult_t st = async_state(m, &bad);
+        if (st != ncclSuccess && st != ncclInProgress) {
+            abort_all(m);
+            return cfail(m, HG_E_COMM, "%s: RCCL error on rank %d: %s (communicator aborted)", what, bad,
+                         ncclGetErrorString(st));
+        }
+        if (armed && Clock::now() > deadline) {
+            if (m->transport == HG_COMM_RCCL) abort_all(m);
+            return cfail(m, HG_E_COMM, "%s: not complete %lld ms after this process's renders retired (a peer rank "
+                                       "missing or stalled?)%s", what, (long long)m->timeout_ms,
+                         m->transport == HG_COMM_RCCL ? "; communicator aborted" : "");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
 }
 
 int ensure_buf(hg_comm* m, DevBuf& b, size_t bytes) {
@@ -84,7 +200,13 @@ int ensure_buf(hg_comm* m, DevBuf& b, size_t bytes) {
     return HG_OK;
 }
 
-// Every member context must be tiled as (its rank, n_ranks) and hold a target of the same size.
+// A member context's own view: tiled as (its rank, n_ranks) with a target.  0 = consistent.
+int member_mismatch(const hg_comm* m, const hg_comm::Member& mb) {
+    const hg_ctx* c = mb.ctx;
+    return (c->n_ranks != m->n_ranks || c->rank != mb.rank || c->W <= 0) ? 1 : 0;
+}
+
+// Every member context must be tiled as (its rank, n_ranks) and hold a target of the same size (in-process check).
 int check_member(hg_comm* m, const hg_comm::Member& mb, int32_t W, int32_t H) {
     const hg_ctx* c = mb.ctx;
     if (c->n_ranks != m->n_ranks || c->rank != mb.rank)
@@ -96,21 +218,96 @@ int check_member(hg_comm* m, const hg_comm::Member& mb, int32_t W, int32_t H) {
     return HG_OK;
 }
 
+// RCCL transport: every rank of the communicator contributes (W, H, -W, -H, bad) and max-reduces; all ranks then hold
+// the same verdict, so a mismatch fails the gather everywhere before any send / receive is posted.
+int agree_on_target(hg_comm* m, int32_t& W, int32_t& H) {
+    for (auto& mb : m->members) {
+        const hg_ctx* c = mb.ctx;
+        int32_t* v = mb.agree_host;
+        v[0] = c->W;
+        v[1] = c->H;
+        v[2] = -c->W;
+        v[3] = -c->H;
+        v[4] = member_mismatch(m, mb);
+        HG_CHIP(m, hipSetDevice(c->device));
+        HG_CHIP(m, hipEventRecord(mb.ready, c->stream));
+        HG_CHIP(m, hipMemcpyAsync(mb.agree_dev, v, kAgreeInts * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    }
+    ncclResult_t gr = ncclGroupStart();
+    if (gr != ncclSuccess) return cfail(m, HG_E_COMM, "ncclGroupStart failed: %s", ncclGetErrorString(gr));
+    ncclResult_t first = ncclSuccess;
+    for (auto& mb : m->members) {
+        const ncclResult_t r =
+            ncclAllReduce(mb.agree_dev, mb.agree_dev, kAgreeInts, ncclInt32, ncclMax, mb.nccl, mb.ctx->stream);
+        if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) first = r;
+    }
+    gr = ncclGroupEnd();  // always closes the group, also after a failed enqueue
+    if (first != ncclSuccess) {
+        abort_all(m);
+        return cfail(m, HG_E_COMM, "ncclAllReduce (gather agreement) failed: %s", ncclGetErrorString(first));
+    }
+    if (gr == ncclInProgress) {
+        if (int rc = wait_comms_ready(m, "gather agreement")) return rc;
+    } else if (gr != ncclSuccess) {
+        abort_all(m);
+        return cfail(m, HG_E_COMM, "ncclGroupEnd (gather agreement) failed: %s", ncclGetErrorString(gr));
+    }
+    for (auto& mb : m->members) {
+        HG_CHIP(m, hipSetDevice(mb.ctx->device));
+        HG_CHIP(m, hipMemcpyAsync(mb.agree_host + kAgreeInts, mb.agree_dev, kAgreeInts * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, mb.ctx->stream));
+    }
+    if (int rc = wait_streams(m, "gather agreement")) return rc;
+    const int32_t* r = m->members.front().agree_host + kAgreeInts;
+    if (r[4] != 0) {
+        for (auto& mb : m->members)
+            if (member_mismatch(m, mb))
+                return cfail(m, HG_E_COMM, "context of rank %d is tiled as %d/%d (target %dx%d), not %d/%d", mb.rank,
+                             mb.ctx->rank, mb.ctx->n_ranks, mb.ctx->W, mb.ctx->H, mb.rank, m->n_ranks);
+        return cfail(m, HG_E_COMM, "a peer rank's context is not tiled for this communicator or has no target");
+    }
+    if (r[0] != -r[2] || r[1] != -r[3])
+        return cfail(m, HG_E_COMM, "ranks disagree on the target size (widths %d..%d, heights %d..%d)", -r[2], r[0],
+                     -r[3], r[1]);
+    W = r[0];
+    H = r[1];
+    return HG_OK;
+}
+
+// Release the staging buffers on the device that holds them, after that device's work on them has retired.
+void free_staging(hg_comm* m) {
+    if (m->buf_device >= 0 && (m->slabs.p || m->image.p)) {
+        (void)hipSetDevice(m->buf_device);
+        if (m->root_ctx) (void)hipStreamSynchronize(m->root_ctx->stream);
+        (void)hipDeviceSynchronize();
+        for (DevBuf* b : {&m->slabs, &m->image}) {
+            if (b->p) (void)hipFree(b->p);
+            *b = DevBuf{};
+        }
+    }
+    m->buf_device = -1;
+}
+
+int alloc_member_rccl(hg_comm* m, hg_comm::Member& mb) {
+    HG_CHIP(m, hipSetDevice(mb.ctx->device));
+    HG_CHIP(m, hipEventCreateWithFlags(&mb.ready, hipEventDisableTiming));
+    HG_CHIP(m, hipMalloc(reinterpret_cast<void**>(&mb.agree_dev), 64));
+    HG_CHIP(m, hipHostMalloc(reinterpret_cast<void**>(&mb.agree_host), 2 * kAgreeInts * sizeof(int32_t), 0));
+    return HG_OK;
+}
+
 }  // namespace
 
-// Row-major image from the root's own accumulator (tiles of the root rank) and the received slabs (other ranks):
-// global tile g = (y/8)*tiles_x + x/8 lives on rank g % n at local slot g / n, pixel (x&7) + 8*(y&7) of it.
+// Row-major image from the root's own accumulator (tiles of the root rank) and the received slabs (other ranks),
+// through the mapping of hg_tiling.h.
 __global__ __launch_bounds__(256) void hg_assemble_image(float4* __restrict__ image, const float4* __restrict__ own,
                                                          const float4* __restrict__ slabs, int32_t W, int32_t H,
                                                          int32_t tiles_x, int32_t n, int32_t root,
                                                          uint32_t slab_tiles) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= uint32_t(W) * uint32_t(H)) return;
-    const uint32_t x = i % uint32_t(W), y = i / uint32_t(W);
-    const uint32_t g = (y >> 3) * uint32_t(tiles_x) + (x >> 3);
-    const uint32_t r = g % uint32_t(n), l = g / uint32_t(n);
-    const size_t lane = (x & 7u) + 8u * (y & 7u);
-    image[i] = r == uint32_t(root) ? own[size_t(l) * 64 + lane] : slabs[(size_t(r) * slab_tiles + l) * 64 + lane];
+    const HgPixelSource s = hg_pixel_source(i % uint32_t(W), i / uint32_t(W), uint32_t(tiles_x), uint32_t(n));
+    image[i] = s.rank == uint32_t(root) ? own[size_t(s.local_tile) * 64u + s.lane] : slabs[hg_slab_index(s, slab_tiles)];
 }
 
 extern "C" {
@@ -131,22 +328,35 @@ int hg_comm_init_rank(hg_ctx* ctx, int32_t n_ranks, const uint8_t id[HG_COMM_ID_
     hg_comm* m = new hg_comm();
     m->n_ranks = n_ranks;
     m->transport = HG_COMM_RCCL;
-    hg_comm::Member mb;
+    m->timeout_ms = env_timeout_ms();
+    m->members.resize(1);
+    hg_comm::Member& mb = m->members.front();
     mb.ctx = ctx;
     mb.rank = rank;
     ncclUniqueId u;
     std::memcpy(u.internal, id, HG_COMM_ID_BYTES);
-    if (hipSetDevice(ctx->device) != hipSuccess) {
-        delete m;
-        return HG_E_HIP;
+    if (int rc = alloc_member_rccl(m, mb)) {
+        ctx->err = m->err;
+        hg_comm_destroy(m);
+        return rc;
     }
-    const ncclResult_t r = ncclCommInitRank(&mb.nccl, n_ranks, u, rank);
-    if (r != ncclSuccess) {
-        ctx->err = std::string("ncclCommInitRank failed: ") + ncclGetErrorString(r);
-        delete m;
-        return HG_E_COMM;
+    // non-blocking: the call returns while the ranks bootstrap; wait_comms_ready bounds the wait for the peers
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&mb.nccl, n_ranks, u, rank, &cfg);
+    int rc = HG_OK;
+    if (r != ncclSuccess && r != ncclInProgress) {
+        rc = cfail(m, HG_E_COMM, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(r));
+        if (mb.nccl) (void)ncclCommAbort(mb.nccl);
+        mb.nccl = nullptr;
+    } else {
+        rc = wait_comms_ready(m, "ncclCommInitRankConfig");
     }
-    m->members.push_back(mb);
+    if (rc != HG_OK) {
+        ctx->err = m->err;
+        hg_comm_destroy(m);
+        return rc;
+    }
     *out = m;
     return HG_OK;
 }
@@ -165,6 +375,7 @@ int hg_comm_init_all(hg_ctx* const* ctxs, int32_t n_ranks, hg_comm** out) {
     hg_comm* m = new hg_comm();
     m->n_ranks = n_ranks;
     m->transport = distinct ? HG_COMM_RCCL : HG_COMM_PEER;
+    m->timeout_ms = env_timeout_ms();
     m->members.resize(size_t(n_ranks));
     std::vector<ncclComm_t> comms(size_t(n_ranks), nullptr);
     if (distinct) {
@@ -180,62 +391,92 @@ int hg_comm_init_all(hg_ctx* const* ctxs, int32_t n_ranks, hg_comm** out) {
         mb.ctx = ctxs[r];
         mb.rank = r;
         mb.nccl = comms[size_t(r)];
-        if (!distinct) {
-            if (hipSetDevice(mb.ctx->device) != hipSuccess ||
-                hipEventCreateWithFlags(&mb.done, hipEventDisableTiming) != hipSuccess) {
-                hg_comm_destroy(m);
-                return HG_E_HIP;
-            }
+        int rc = HG_OK;
+        if (distinct) {
+            rc = alloc_member_rccl(m, mb);
+        } else if (hipSetDevice(mb.ctx->device) != hipSuccess ||
+                   hipEventCreateWithFlags(&mb.done, hipEventDisableTiming) != hipSuccess) {
+            rc = HG_E_HIP;
+        }
+        if (rc != HG_OK) {
+            ctxs[0]->err = m->err.empty() ? "hg_comm_init_all: HIP setup failed" : m->err;
+            hg_comm_destroy(m);
+            return rc;
         }
     }
     *out = m;
     return HG_OK;
 }
 
+int hg_comm_set_timeout_ms(hg_comm* m, int64_t timeout_ms) {
+    if (!m) return HG_E_INVALID;
+    if (timeout_ms <= 0) return cfail(m, HG_E_INVALID, "timeout must be > 0 ms");
+    m->timeout_ms = timeout_ms;
+    return HG_OK;
+}
+
 int hg_comm_gather(hg_comm* m, int32_t root) {
     if (!m) return HG_E_INVALID;
+    if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
     if (root < 0 || root >= m->n_ranks) return cfail(m, HG_E_INVALID, "root %d out of range", root);
+    int32_t W = m->members.front().ctx->W, H = m->members.front().ctx->H;
+    if (m->transport == HG_COMM_RCCL) {
+        if (int rc = agree_on_target(m, W, H)) return rc;
+    } else {
+        for (const auto& mb : m->members)
+            if (int rc = check_member(m, mb, W, H)) return rc;
+    }
     const hg_ctx* c0 = m->members.front().ctx;
-    const int32_t W = c0->W, H = c0->H;
-    for (const auto& mb : m->members)
-        if (int rc = check_member(m, mb, W, H)) return rc;
     const int32_t n = m->n_ranks;
     const int64_t total = int64_t(c0->tiles_x) * c0->tiles_y;
-    const int64_t slab_tiles = local_tiles(total, 0, n);  // rank 0 holds the most tiles
+    const int64_t slab_tiles = hg_rank_tiles(total, 0, n);  // rank 0 holds the most tiles
     const size_t slab_floats = size_t(slab_tiles) * 64 * 4;
     hg_comm::Member* rootm = nullptr;
     for (auto& mb : m->members)
         if (mb.rank == root) rootm = &mb;
     if (rootm) {  // this process holds the root: staging slabs and the image on its device
+        if (m->buf_device != rootm->ctx->device) free_staging(m);  // a root on another device: its own staging
         HG_CHIP(m, hipSetDevice(rootm->ctx->device));
-        if (m->buf_device != rootm->ctx->device) {  // a root on another device: its own staging
-            HG_CHIP(m, hipDeviceSynchronize());
-            for (DevBuf* b : {&m->slabs, &m->image}) {
-                if (b->p) (void)hipFree(b->p);
-                *b = DevBuf{};
-            }
-            m->buf_device = rootm->ctx->device;
-        }
+        m->buf_device = rootm->ctx->device;
         if (int rc = ensure_buf(m, m->slabs, size_t(n) * slab_floats * sizeof(float))) return rc;
         if (int rc = ensure_buf(m, m->image, size_t(W) * size_t(H) * sizeof(float4))) return rc;
     }
     m->root = -1;  // valid again once the assembly is enqueued
     if (m->transport == HG_COMM_RCCL) {
-        HG_CNCCL(m, ncclGroupStart());
+        ncclResult_t gr = ncclGroupStart();
+        if (gr != ncclSuccess) return cfail(m, HG_E_COMM, "ncclGroupStart failed: %s", ncclGetErrorString(gr));
+        ncclResult_t first = ncclSuccess;
+        const char* first_what = "";
+        auto note = [&](ncclResult_t r, const char* what) {
+            if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
+                first = r;
+                first_what = what;
+            }
+        };
         for (auto& mb : m->members) {
-            const size_t cnt = size_t(local_tiles(total, mb.rank, n)) * 64 * 4;
+            const size_t cnt = size_t(hg_rank_tiles(total, mb.rank, n)) * 64 * 4;
             if (mb.rank == root) {
                 for (int32_t r = 0; r < n; ++r) {
-                    const size_t rc = size_t(local_tiles(total, r, n)) * 64 * 4;
+                    const size_t rc = size_t(hg_rank_tiles(total, r, n)) * 64 * 4;
                     if (r == root || rc == 0) continue;
                     float* dst = static_cast<float*>(m->slabs.p) + size_t(r) * slab_floats;
-                    HG_CNCCL(m, ncclRecv(dst, rc, ncclFloat32, r, mb.nccl, mb.ctx->stream));
+                    note(ncclRecv(dst, rc, ncclFloat32, r, mb.nccl, mb.ctx->stream), "ncclRecv");
                 }
             } else if (cnt) {
-                HG_CNCCL(m, ncclSend(mb.ctx->acc.p, cnt, ncclFloat32, root, mb.nccl, mb.ctx->stream));
+                note(ncclSend(mb.ctx->acc.p, cnt, ncclFloat32, root, mb.nccl, mb.ctx->stream), "ncclSend");
             }
         }
-        HG_CNCCL(m, ncclGroupEnd());
+        gr = ncclGroupEnd();  // always closes the group, also after a failed enqueue
+        if (first != ncclSuccess) {
+            abort_all(m);
+            return cfail(m, HG_E_COMM, "%s failed: %s (communicator aborted)", first_what, ncclGetErrorString(first));
+        }
+        if (gr == ncclInProgress) {
+            if (int rc = wait_comms_ready(m, "gather send/recv group")) return rc;
+        } else if (gr != ncclSuccess) {
+            abort_all(m);
+            return cfail(m, HG_E_COMM, "ncclGroupEnd failed: %s (communicator aborted)", ncclGetErrorString(gr));
+        }
     } else {  // peer transport: every member is in this process and rootm is set
         // the slabs are free once the root's previous assembly has read them
         HG_CHIP(m, hipEventRecord(rootm->done, rootm->ctx->stream));
@@ -243,7 +484,7 @@ int hg_comm_gather(hg_comm* m, int32_t root) {
             if (mb.rank == root) continue;
             HG_CHIP(m, hipSetDevice(mb.ctx->device));
             HG_CHIP(m, hipStreamWaitEvent(mb.ctx->stream, rootm->done, 0));
-            const size_t bytes = size_t(local_tiles(total, mb.rank, n)) * 64 * sizeof(float4);
+            const size_t bytes = size_t(hg_rank_tiles(total, mb.rank, n)) * 64 * sizeof(float4);
             if (bytes) {
                 float* dst = static_cast<float*>(m->slabs.p) + size_t(mb.rank) * slab_floats;
                 HG_CHIP(m, hipMemcpyPeerAsync(dst, rootm->ctx->device, mb.ctx->acc.p, mb.ctx->device, bytes,
@@ -270,10 +511,18 @@ int hg_comm_gather(hg_comm* m, int32_t root) {
     return HG_OK;
 }
 
+int hg_comm_synchronize(hg_comm* m) {
+    if (!m) return HG_E_INVALID;
+    if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
+    return wait_streams(m, "hg_comm_synchronize");
+}
+
 int hg_comm_readback(hg_comm* m, float* rgba, size_t n_floats) {
     if (!m || !rgba) return HG_E_INVALID;
+    if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
     if (m->root < 0 || !m->root_ctx) return cfail(m, HG_E_INVALID, "no gathered image in this process");
     if (n_floats < size_t(m->W) * size_t(m->H) * 4) return cfail(m, HG_E_INVALID, "readback buffer too small");
+    if (int rc = wait_streams(m, "hg_comm_readback")) return rc;  // the receives, bounded by the deadline
     hg_ctx* rc = m->root_ctx;
     HG_CHIP(m, hipSetDevice(rc->device));
     HG_CHIP(m, hipMemcpyAsync(rgba, m->image.p, size_t(m->W) * size_t(m->H) * sizeof(float4), hipMemcpyDeviceToHost,
@@ -289,17 +538,36 @@ const char* hg_comm_last_error(const hg_comm* m) { return m ? m->err.c_str() : "
 void hg_comm_destroy(hg_comm* m) {
     if (!m) return;
     for (auto& mb : m->members) {
-        if (mb.ctx) {
+        // after an abort a member stream may hold an RCCL kernel of the aborted comm: do not wait on it
+        if (mb.ctx && !m->aborted) {
             (void)hipSetDevice(mb.ctx->device);
             (void)hipStreamSynchronize(mb.ctx->stream);
         }
         if (mb.nccl) (void)ncclCommDestroy(mb.nccl);
         if (mb.done) (void)hipEventDestroy(mb.done);
+        if (mb.ready) (void)hipEventDestroy(mb.ready);
+        if (mb.agree_dev) (void)hipFree(mb.agree_dev);
+        if (mb.agree_host) (void)hipHostFree(mb.agree_host);
     }
-    if (m->root_ctx) (void)hipSetDevice(m->root_ctx->device);
-    if (m->slabs.p) (void)hipFree(m->slabs.p);
-    if (m->image.p) (void)hipFree(m->image.p);
+    if (!m->aborted) free_staging(m);
     delete m;
+}
+
+// Host twin of hg_assemble_image over the [rank][slab_tiles][64] float4 layout (slab r = rank r's local tiles, the
+// root's own included): the torch all_gather path (halogen/distributed.py) and the CPU tests use it.  No device work.
+int hg_comm_assemble_host(const float* slabs, int64_t slab_tiles, int32_t width, int32_t height, int32_t n_ranks,
+                          float* rgba, size_t n_floats) {
+    if (!slabs || !rgba || width <= 0 || height <= 0 || n_ranks < 1) return HG_E_INVALID;
+    const int64_t tiles_x = (width + HG_TILE - 1) / HG_TILE, tiles_y = (height + HG_TILE - 1) / HG_TILE;
+    if (slab_tiles < hg_rank_tiles(tiles_x * tiles_y, 0, n_ranks)) return HG_E_INVALID;
+    if (n_floats < size_t(width) * size_t(height) * 4) return HG_E_INVALID;
+    for (int32_t y = 0; y < height; ++y)
+        for (int32_t x = 0; x < width; ++x) {
+            const HgPixelSource s = hg_pixel_source(uint32_t(x), uint32_t(y), uint32_t(tiles_x), uint32_t(n_ranks));
+            std::memcpy(rgba + (size_t(y) * size_t(width) + size_t(x)) * 4,
+                        slabs + hg_slab_index(s, uint32_t(slab_tiles)) * 4, 4 * sizeof(float));
+        }
+    return HG_OK;
 }
 
 }  // extern "C"

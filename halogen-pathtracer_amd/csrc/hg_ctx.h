@@ -47,7 +47,9 @@ struct hg_ctx {
     DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     DevBuf pool;                 // path-pool kernel: per-wave path slots
     DevBuf tile_cost, tile_order;  // cost-ordered dispatch: per local tile, wave-clock cost / dispatch order
-    bool tile_cost_valid = false;  // tile_cost holds the previous regen/stream launch's costs for this tiling
+    bool tile_cost_valid = false;  // tile_cost holds the costs recorded since the last sort, for this tiling
+    bool tile_order_valid = false;  // tile_order holds a sorted order for this tiling
+    int64_t frames_since_order = 0;  // frames whose wave times tile_cost has accumulated since the last sort
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;

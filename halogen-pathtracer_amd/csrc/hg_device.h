@@ -582,7 +582,10 @@ struct LeafRay {  // the lane's side of a leaf test: its mesh-local ray and runn
 __device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRay& t, Counters& c, const LeafShare& ls,
                                           uint32_t first, uint32_t n) {
 #if HG_CHECK_EXEC
-    if (__ballot(1) != ~0ull) return false;  // partial EXEC: the sequential loop instead (see above)
+    if (__ballot(1) != ~0ull) {  // partial EXEC: the sequential loop instead (see above), counted in counter slot 17
+        if (kp.counters) atomicAdd(kp.counters + 17, 1ull);
+        return false;
+    }
 #endif
     const uint32_t lane = __lane_id();
     const uint32_t incl = wave_incl_add(n);

@@ -119,9 +119,11 @@
 #ifndef HG_PHASE_DETAIL
 #define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
 #endif
-#ifndef HG_LDS_ACC
-#define HG_LDS_ACC 1  // streaming kernel, spp 1 and unsplit: the lane's accumulator lives in LDS for the launch
-#endif
+// (HG_LDS_ACC, the round-2 LDS accumulator of unsplit per-pixel-lane launches, is gone: the item scheduling replaced
+// those launches.  A 1-frame launch now blends straight into the accumulator, hg_mega.hip.)
+#ifndef HG_ORDER_MIN_FRAMES
+#define HG_ORDER_MIN_FRAMES 16  // hg_render re-sorts the tile order once at least this many frames of costs were recorded
+#endif                          // since the last sort (64-frame launches: every launch; 1-frame launches: every 16th)
 #ifndef HG_NODE_CACHE
 #define HG_NODE_CACHE 0  // streaming kernel: the top records of every BLAS (BFS) copied into LDS per wave (records,
 #endif                   // a multiple of 4: 4 records = one 64-lane LDS row)

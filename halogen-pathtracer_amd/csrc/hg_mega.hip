@@ -87,14 +87,11 @@ size_t hg_mega_lds_bytes(uint32_t stack_depth, int block) {
 // Per-lane path state parked in LDS (RowVec3 / RowVec4 rows, hg_device.h): the throughput, radiance and sample sum
 // are touched once per bounce, so they stay out of the registers the traversal needs.
 constexpr uint32_t kRegenLdsState = 9;  // words per lane: throughput, radiance, sample sum
-// Streaming kernel: one more word per lane.  With spp == 1 and an unsplit launch the sample sum is never needed
-// (the frame's colour is the path's colour), and its 3 words plus the extra one hold the lane's accumulator value
-// for the whole launch (HG_LDS_ACC): the per-frame blend acc*(1-w) + c*w reads and writes LDS instead of a global
-// read-modify-write per pixel-frame; the value comes from global memory once at the wave's start and goes back once
-// at its end.  Same operations in the same order: bit-identical.
+// Streaming kernel: one more word per lane (row 9, unused since the round-2 LDS accumulator was retired: the leaf-share
+// rows stay 64-bit aligned at row 10).
 constexpr uint32_t kStreamLdsState = 10;
 // Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
-// 6-8 or the accumulator 6-9 (lds_acc), the distributed leaf test 10-12, the traversal stack from row 13.
+// 6-8, the distributed leaf test 10-12, the traversal stack from row 13.
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
 constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
 static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
@@ -409,7 +406,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
-                    if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
+                    if (split > 1u || (HG_REGEN_ITEMS && kp.n_frames > 1)) {  // colour, blended later in frame order
                         kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
@@ -604,7 +601,7 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp_in, int block, bool cou
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
-template <bool kCounters, bool kLdsAcc, bool kMeshLds>
+template <bool kCounters, bool kMeshLds>
 __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
@@ -621,10 +618,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     const RowVec3<kRowThr> s_thr{lane};
     const RowVec3<kRowCol> s_col{lane};
     const RowVec3<kRowSum> s_sum{lane};
-    const RowVec4<kRowSum> s_acc{lane};  // the sum's words (+1): used only when lds_acc
     const LeafShare ls{kRowLeaf * 64u};
     const uint32_t nm = uint32_t(kp.n_meshes);
-    constexpr bool lds_acc = kLdsAcc;  // launched only with spp == 1 and frame_split == 1 (hg_launch_mega_stream)
     if (kMeshLds) {  // the wave's copy of the mesh records (mesh_f4, hg_device.h)
         mesh_lds_fill(kp, lane);
         wave_lds_sync();
@@ -675,8 +670,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         paths++;
         s_thr.set(mk(1, 1, 1));
         s_col.set(mk(0, 0, 0));
-        if (lds_acc) s_acc.set(kp.acc[size_t(uint32_t(local_tile)) * 64u + lane]);
-        else s_sum.set(mk(0, 0, 0));
+        s_sum.set(mk(0, 0, 0));
         trav_begin<kMeshLds>(kp, ray, tv, c);
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
@@ -747,20 +741,23 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             if (kCounters) tp = phase_mark(kp, 12, tp);
 #endif
             if (!alive) {
-                // RayColor += trace_ray(...); with lds_acc (spp 1) the sum is the path's colour (0 + col == col)
-                // (col is never -0: it starts at +0 and only has terms added, so 0 + col == col bit for bit)
-                const bool one_sample = lds_acc || kp.spp == 1;
+                // RayColor += trace_ray(...); spp 1: the sum is the path's colour (0 + col == col bit for bit: col
+                // is never -0, it starts at +0 and only has terms added)
+                const bool one_sample = kp.spp == 1;
                 f3 sum = one_sample ? col : s_sum.get() + col;
                 ++fs;
                 bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
-                    if (HG_STREAM_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
+                    // A multi-frame launch stores this frame's colour, blended later in frame order (hg_blend_frames);
+                    // a 1-frame launch (the reference's one dispatch per frame, RP:327) has one item per pixel and
+                    // blends it straight into the accumulator: the same operations, no colour buffer, no blend pass.
+                    if (split > 1u || (HG_STREAM_ITEMS && kp.n_frames > 1)) {
                         kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
-                        float4 acc = lds_acc ? s_acc.get() : kp.acc[slot_i];
+                        float4 acc = kp.acc[slot_i];
                         if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
                             const float w = rcp_exact(float(smp.frame));
                             const float k = 1.0f - w;
@@ -769,8 +766,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                         } else {
                             acc = make_float4(color.x, color.y, color.z, 1.0f);
                         }
-                        if (lds_acc) s_acc.set(acc);
-                        else kp.acc[slot_i] = acc;
+                        kp.acc[slot_i] = acc;
                     }
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
 #if HG_STREAM_ITEMS
@@ -835,8 +831,6 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #endif
         if (kCounters) cyc_shade += wave_clock();
     }
-    if (lds_acc && fs >= 0x10000u)  // unsplit: a lane that traced its pixel ended on frame f_end > f_begin = 0
-        kp.acc[size_t(uint32_t(local_tile)) * 64u + lane] = s_acc.get();
     record_tile_cost(lane);
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
@@ -857,14 +851,6 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     }
 }
 
-template <bool kCounters, bool kLdsAcc>
-static void launch_stream(const HgKernelParams& kp, uint32_t grid, size_t lds, size_t mesh_lds, hipStream_t stream) {
-    if (mesh_lds)
-        hipLaunchKernelGGL((hg_trace_stream_kernel<kCounters, kLdsAcc, true>), dim3(grid), dim3(64), mesh_lds, stream, kp);
-    else
-        hipLaunchKernelGGL((hg_trace_stream_kernel<kCounters, kLdsAcc, false>), dim3(grid), dim3(64), lds, stream, kp);
-}
-
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
     const int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
@@ -874,12 +860,11 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     HgKernelParams kp = kp_in;
     kp.mesh_lds_word = uint32_t(lds / 4u);
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
-    const bool lds_acc = HG_LDS_ACC && !HG_STREAM_ITEMS && kp.spp == 1u && kp.frame_split == 1;
-    const uint32_t g = uint32_t(grid);
-    if (counters && lds_acc) launch_stream<true, true>(kp, g, lds, mesh_lds, stream);
-    else if (counters) launch_stream<true, false>(kp, g, lds, mesh_lds, stream);
-    else if (lds_acc) launch_stream<false, true>(kp, g, lds, mesh_lds, stream);
-    else launch_stream<false, false>(kp, g, lds, mesh_lds, stream);
+    const dim3 g{uint32_t(grid)}, b{64u};
+    if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), g, b, mesh_lds, stream, kp);
+    else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), g, b, lds, stream, kp);
+    else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), g, b, mesh_lds, stream, kp);
+    else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
 

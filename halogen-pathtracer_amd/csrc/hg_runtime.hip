@@ -274,6 +274,7 @@ int alloc_target(hg_ctx* c) {
     const int64_t total = int64_t(c->tiles_x) * c->tiles_y;
     c->n_local_tiles = total > c->rank ? int32_t((total - c->rank + c->n_ranks - 1) / c->n_ranks) : 0;
     c->tile_cost_valid = false;
+    c->tile_order_valid = false;
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     const size_t slots = size_t(c->n_local_tiles) * 64;
 #if HG_WITH_VARIANTS  // wavefront pipeline path state (152 B per pixel slot)
@@ -817,9 +818,10 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         }
         if (units > 0) split = int(std::min<int64_t>(split, kMaxWaves / units));
         int chunk_max = HG_REGEN_MAX_CHUNK;
-        // frame colours, blended after the launch (frame split, or item scheduling)
+        // frame colours, blended after the launch (frame split, or item scheduling of a multi-frame launch; a 1-frame
+        // launch blends each pixel's one item straight into the accumulator)
         const bool items_k = regen && !pool_k && (stream_k ? HG_STREAM_ITEMS : HG_REGEN_ITEMS);
-        const bool colours = split > 1 || items_k;
+        const bool colours = split > 1 || (items_k && n_frames > 1);
         if (colours) {
             const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
             chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
@@ -873,20 +875,30 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
                 if (kc.tile_cost) {
-                    if (c->tile_cost_valid) {  // order from the recorded costs, which it then clears
+                    // Sort from the recorded costs (which the sort clears) once HG_ORDER_MIN_FRAMES frames' worth have
+                    // accumulated, or when no order exists yet; in between, launches keep the last order and add to
+                    // the costs.  A 64-frame launch sorts every time; the drop-in's 1-frame launches (RP:327) pay the
+                    // 0.1-ms sort once per 16 frames instead of once per frame.
+                    if (c->tile_cost_valid &&
+                        (!c->tile_order_valid || c->frames_since_order >= int64_t(HG_ORDER_MIN_FRAMES))) {
                         e = hg_launch_order_tiles(kc.tile_cost, static_cast<uint32_t*>(c->tile_order.p),
                                                   uint32_t(tiles), c->stream);
-                        kc.tile_order = static_cast<const uint32_t*>(c->tile_order.p);
-                    } else {
+                        c->tile_order_valid = e == hipSuccess;
+                        c->frames_since_order = 0;
+                    } else if (!c->tile_cost_valid) {
                         e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(unsigned long long), c->stream);
+                        c->tile_order_valid = false;
+                        c->frames_since_order = 0;
                     }
+                    if (c->tile_order_valid) kc.tile_order = static_cast<const uint32_t*>(c->tile_order.p);
                     c->tile_cost_valid = e == hipSuccess;
+                    c->frames_since_order += kc.n_frames;
                 }
                 if (e == hipSuccess)
                     e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
                     : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
                                : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
-                if (e == hipSuccess && (kc.frame_split > 1 || items_k))
+                if (e == hipSuccess && (kc.frame_split > 1 || (items_k && kc.n_frames > 1)))
                     e = hg_launch_blend_frames(kc, c->stream);
                 done += kc.n_frames;
             }
@@ -950,6 +962,31 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
     return HG_OK;
 }
 
+int hg_set_accumulation(hg_ctx* c, const float* rgba, size_t n_floats, int32_t frame_count) {
+    if (!c || !rgba) return HG_E_INVALID;
+    if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
+    if (n_floats < size_t(c->W) * size_t(c->H) * 4) return fail(c, HG_E_INVALID, "accumulation image too small");
+    if (frame_count < 1) return fail(c, HG_E_INVALID, "frame_count must be >= 1 (FrameCount starts at 1, RP:152)");
+    if (int rc = set_device(c)) return rc;
+    // the tile-major repack of hg_readback, inverted; slots of an edge tile outside the image hold 0, as after a clear
+    std::vector<float4> tiles(size_t(c->n_local_tiles) * 64, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (int32_t lt = 0; lt < c->n_local_tiles; ++lt) {
+        const int64_t gt = int64_t(c->rank) + int64_t(lt) * c->n_ranks;
+        const int tx = int(gt % c->tiles_x), ty = int(gt / c->tiles_x);
+        for (int l = 0; l < 64; ++l) {
+            const int x = tx * HG_TILE + (l & 7), y = ty * HG_TILE + (l >> 3);
+            if (x >= c->W || y >= c->H) continue;
+            const float* s = rgba + (size_t(y) * c->W + x) * 4;
+            tiles[size_t(lt) * 64 + l] = make_float4(s[0], s[1], s[2], s[3]);
+        }
+    }
+    if (!tiles.empty())
+        HG_HIP(c, hipMemcpyAsync(c->acc.p, tiles.data(), tiles.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HG_HIP(c, hipStreamSynchronize(c->stream));  // the staging vector dies at return
+    c->params.frameCount = frame_count;
+    return drain_events(c);
+}
+
 int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
     if (!c || !dst) return HG_E_INVALID;
     const size_t need = size_t(c->n_local_tiles) * 64 * sizeof(float4);
@@ -984,6 +1021,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     for (int k = 0; k < 4; ++k) out->shade_detail[k] = v[11 + k];
     out->shade_rounds = v[15];
     out->primary_misses = v[16];
+    out->exec_fallbacks = v[17];
     return HG_OK;
 }
 
@@ -1000,6 +1038,10 @@ int hg_reset_counters(hg_ctx* c) {
 int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
     if (!c) return HG_E_INVALID;
     if (int rc = set_device(c)) return rc;
+    if (test == HG_SELFTEST_BUILD) {  // compile-time checks of this build (no device work)
+        if (tested) *tested = 0;
+        return HG_CHECK_EXEC ? HG_BUILD_CHECK_EXEC : 0;
+    }
     if (test != HG_SELFTEST_RCP) return fail(c, HG_E_INVALID, "unknown self-test %d", test);
     const int64_t r = hg_selftest_rcp_all(tested);
     if (r < 0) return fail(c, HG_E_HIP, "self-test failed to run");
@@ -1038,6 +1080,7 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_TILE_ORDER:
             c->tile_order_on = value ? 1 : 0;
             c->tile_cost_valid = false;
+            c->tile_order_valid = false;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

@@ -81,7 +81,8 @@ class HgCounters(C.Structure):
                 ("trace_ms", C.c_double), ("trace_launches", C.c_uint64), ("node_rounds", C.c_uint64),
                 ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64),
                 ("trace_cycles", C.c_uint64), ("shade_cycles", C.c_uint64),
-                ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64)]
+                ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64),
+                ("exec_fallbacks", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)
@@ -99,14 +100,17 @@ HG_OPT_TILE_ORDER = 8
 EXPORTS = [
     "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
-    "hg_readback", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
+    "hg_readback", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
     "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
-    "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_readback",
-    "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
+    "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_synchronize",
+    "hg_comm_readback", "hg_comm_set_timeout_ms", "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
+    "hg_comm_assemble_host",
 ]
 HG_COMM_ID_BYTES = 128
 HG_COMM_RCCL, HG_COMM_PEER = 1, 2
 HG_SELFTEST_RCP = 1
+HG_SELFTEST_BUILD = 2
+HG_BUILD_CHECK_EXEC = 1
 
 _lib = None
 
@@ -135,6 +139,7 @@ def lib() -> C.CDLL:
         "hg_render": (C.c_int, [P, i32, i32]),
         "hg_synchronize": (C.c_int, [P]),
         "hg_readback": (C.c_int, [P, f32p, sz]),
+        "hg_set_accumulation": (C.c_int, [P, f32p, sz, i32]),
         "hg_copy_tiles_device": (C.c_int, [P, P, sz]),
         "hg_local_tile_count": (i32, [P]),
         "hg_get_counters": (C.c_int, [P, C.POINTER(HgCounters)]),
@@ -149,7 +154,10 @@ def lib() -> C.CDLL:
         "hg_comm_init_rank": (C.c_int, [P, i32, C.c_char_p, i32, C.POINTER(P)]),
         "hg_comm_init_all": (C.c_int, [C.POINTER(P), i32, C.POINTER(P)]),
         "hg_comm_gather": (C.c_int, [P, i32]),
+        "hg_comm_synchronize": (C.c_int, [P]),
         "hg_comm_readback": (C.c_int, [P, f32p, sz]),
+        "hg_comm_set_timeout_ms": (C.c_int, [P, i64]),
+        "hg_comm_assemble_host": (C.c_int, [f32p, i64, i32, i32, i32, f32p, sz]),
         "hg_comm_transport": (C.c_int, [P]),
         "hg_comm_last_error": (C.c_char_p, [P]),
         "hg_comm_destroy": (None, [P]),
@@ -248,6 +256,13 @@ class Context:
         self._check(lib().hg_readback(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size), "hg_readback")
         return out
 
+    def set_accumulation(self, image: np.ndarray, frame_count: int) -> None:
+        """Checkpoint resume (hg_set_accumulation): the (h, w, 4) image hg_readback returned and the FrameCount of
+        the next frame."""
+        img = np.ascontiguousarray(image, dtype=np.float32)
+        self._check(lib().hg_set_accumulation(self._h, img.ctypes.data_as(C.POINTER(C.c_float)), img.size,
+                                              int(frame_count)), "hg_set_accumulation")
+
     def local_tile_count(self) -> int:
         return int(lib().hg_local_tile_count(self._h))
 
@@ -323,6 +338,13 @@ class Comm:
     def gather(self, root: int = 0) -> None:
         self._check(lib().hg_comm_gather(self._h, root), "hg_comm_gather")
 
+    def synchronize(self) -> None:
+        """Wait for this process's part of the last gather, bounded by the deadline (HalogenError on a dead peer)."""
+        self._check(lib().hg_comm_synchronize(self._h), "hg_comm_synchronize")
+
+    def set_timeout_ms(self, ms: int) -> None:
+        self._check(lib().hg_comm_set_timeout_ms(self._h, int(ms)), "hg_comm_set_timeout_ms")
+
     def readback(self, w: int, h: int, out: np.ndarray | None = None) -> np.ndarray:
         if out is None:
             out = np.zeros((h, w, 4), dtype=np.float32)
@@ -346,6 +368,21 @@ class Comm:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def assemble_host(slabs: np.ndarray, width: int, height: int, n_ranks: int) -> np.ndarray:
+    """hg_comm_assemble_host: (n_ranks, slab_tiles, 64, 4) float32 tiles (slab r = rank r's local tiles) -> the
+    (height, width, 4) image, through the mapping the device gather uses (csrc/hg_tiling.h).  Needs no GPU."""
+    s = np.ascontiguousarray(slabs, dtype=np.float32)
+    if s.ndim != 4 or s.shape[0] != n_ranks or s.shape[2:] != (64, 4):
+        raise ValueError(f"slabs must be (n_ranks={n_ranks}, slab_tiles, 64, 4), got {s.shape}")
+    out = np.empty((height, width, 4), np.float32)
+    fp = C.POINTER(C.c_float)
+    rc = lib().hg_comm_assemble_host(s.ctypes.data_as(fp), s.shape[1], width, height, n_ranks, out.ctypes.data_as(fp),
+                                     out.size)
+    if rc != HG_OK:
+        raise HalogenError(f"hg_comm_assemble_host failed ({rc}): slabs {s.shape} for {width}x{height}, {n_ranks} ranks")
+    return out
 
 
 def gpu_available() -> bool:

@@ -4,14 +4,20 @@ Pixels are independent: a pixel's value depends only on the scene, the uniforms,
 FrameCount (HalgoenCompute.compute:1033).  So the image's 8x8 tiles are dealt round-robin to ranks
 (tile t -> rank t % N, which balances the centre-heavy dragon), every rank traces and accumulates all
 frames of its own tiles, and the only collective is one gather of the packed accumulated tiles at the end.
-One process per GPU; torch.distributed is the transport (backend "nccl" = RCCL over xGMI on ROCm, "gloo" in
-CPU tests).  The gathered image is bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
-tests/test_distributed_cpu.py).
+
+This module is the torch.distributed form of that gather (backend "nccl" = RCCL over xGMI on ROCm, "gloo" in the CPU
+tests and the one-GPU rehearsal): one all_gather_into_tensor of every rank's tiles, then the image is assembled on
+the host by hg_comm_assemble_host, the host twin of the C-ABI gather's device assembly (hg_comm_gather), which reads
+pixels through the same tile -> rank / slot / pixel mapping (csrc/hg_tiling.h).  The gathered image is bit-identical
+to a 1-GPU render (tests/test_gpu_parity.py, tests/test_distributed_cpu.py).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
+
+from . import abi
 
 TILE = 8
 
@@ -24,7 +30,7 @@ def local_tile_count(total_tiles: int, rank: int, n_ranks: int) -> int:
     return max(0, (total_tiles - rank + n_ranks - 1) // n_ranks)
 
 
-def gather_tiles(local: torch.Tensor, rank: int, n_ranks: int, width: int, height: int) -> torch.Tensor | None:
+def gather_tiles(local: torch.Tensor, rank: int, n_ranks: int, width: int, height: int) -> np.ndarray | None:
     """local: (n_local_tiles, 64, 4) float32 tiles of this rank (hg_copy_tiles_device layout).
     Returns the (height, width, 4) image on rank 0 (None elsewhere).  One all_gather_into_tensor of
     max-local-tiles x 1 KiB per rank (ranks hold ceil/floor shares, padded to the max)."""
@@ -40,10 +46,8 @@ def gather_tiles(local: torch.Tensor, rank: int, n_ranks: int, width: int, heigh
     return untile(out.view(n_ranks, max_local, 64, 4), n_ranks, width, height)
 
 
-def untile(per_rank: torch.Tensor, n_ranks: int, width: int, height: int) -> torch.Tensor:
-    """(n_ranks, max_local, 64, 4) -> (height, width, 4): global tile g lives at rank g % N, slot g // N."""
-    tx, ty = tiles_xy(width, height)
-    g = torch.arange(tx * ty, device=per_rank.device)
-    tiles = per_rank[g % n_ranks, g // n_ranks]  # (total, 64, 4) in global tile order
-    img = tiles.view(ty, tx, TILE, TILE, 4).permute(0, 2, 1, 3, 4).reshape(ty * TILE, tx * TILE, 4)
-    return img[:height, :width]
+def untile(per_rank, n_ranks: int, width: int, height: int) -> np.ndarray:
+    """(n_ranks, max_local, 64, 4) slabs -> (height, width, 4): global tile g lives at rank g % N, slot g // N
+    (hg_comm_assemble_host, the mapping of the device gather)."""
+    slabs = per_rank.cpu().numpy() if isinstance(per_rank, torch.Tensor) else np.asarray(per_rank)
+    return abi.assemble_host(slabs, width, height, n_ranks)

@@ -215,6 +215,16 @@ class HalogenRenderPass:
         w, h = self._prior_resolution
         return self.ctx.readback(w, h)
 
+    def restore(self, image: np.ndarray, frame_count: int):
+        """Checkpoint resume (not in the reference, whose resumable state is the accumulation RTHandle and the
+        FrameCount field, RP:152,185,347): restore(read_image(), getFrameCount()) on a new pass continues the
+        progressive render bit-identically (hg_set_accumulation)."""
+        h, w = image.shape[:2]
+        self.OnCameraSetup(w, h)
+        self.ctx.set_accumulation(image, frame_count)
+        self.FrameCount = int(frame_count)
+        self.AccumulationBufferDirty = False
+
     def getFrameCount(self) -> int:
         return self.FrameCount
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 2
+#define HG_ABI_VERSION 3
 
 /* ----------------------------------------------------------------------------------------------
  * Reference host structs (byte-identical to the C# [Sequential] structs)
@@ -156,6 +156,9 @@ typedef struct hg_counters {
                               utilisation of shading = rays / (64 * shade_rounds)) */
     uint64_t primary_misses; /* paths whose camera ray hits nothing (trace_ray's first iteration takes the miss branch,
                                 HC:941): a one-ray path; primary_misses / paths is the share of near-free paths */
+    uint64_t exec_fallbacks; /* HG_CHECK_EXEC builds only (hg_selftest HG_SELFTEST_BUILD): lane-events where the
+                                distributed leaf test found a lane of its wave inactive and took the sequential leaf
+                                loop; must stay 0 (its DPP scans need a full wave).  0 in product builds */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -243,6 +246,13 @@ int hg_synchronize(hg_ctx* ctx);
  * rank's pixels are written; the others are left untouched. Blocks. */
 int hg_readback(hg_ctx* ctx, float* rgba, size_t n_floats);
 
+/* Checkpoint / resume: the inverse of hg_readback.  The reference's whole resumable state is the accumulation target
+ * and FrameCount (RP:152, RP:185, RP:347).  Loads a row-major RGBA32F image (width*height*4 floats, as hg_readback
+ * returns it; with tiling only this rank's pixels are read) into the accumulation target and sets the FrameCount the
+ * next accumulated frame is traced with (frame_count >= 1; a later hg_set_params supplies its own frameCount).
+ * readback -> new context -> hg_set_accumulation -> hg_render continues bit-identically.  Blocks. */
+int hg_set_accumulation(hg_ctx* ctx, const float* rgba, size_t n_floats, int32_t frame_count);
+
 /* Device-to-device copy of this rank's packed tiles (n_local_tiles * 64 * 4 floats, tile-major,
  * pixel (lx,ly) of a tile at lx + 8*ly) into caller-owned device memory on the same device.  Returns after the copy
  * has completed on the context stream; a consumer on another stream or engine must order itself after the call.
@@ -256,10 +266,12 @@ int hg_reset_counters(hg_ctx* ctx);
 /* Tuning knobs (kernel variant, block size, counters on/off). */
 int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
 
-/* Device self-tests of arithmetic shortcuts the kernels rely on.  HG_SELFTEST_RCP: the fast correctly-rounded
+/* Device self-tests of arithmetic shortcuts the kernels rely on (and the build's compiled-in checks).  HG_SELFTEST_RCP: the fast correctly-rounded
  * reciprocal against IEEE 1.0f/x for every float of its range.  Returns the number of mismatches (must be 0),
  * or a negative error; *tested (optional) receives the number of inputs checked. */
-enum { HG_SELFTEST_RCP = 1 };
+enum { HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2 };
+/* HG_SELFTEST_BUILD returns a bit mask of the run-time checks compiled into this build (no device work). */
+enum { HG_BUILD_CHECK_EXEC = 1 };
 int64_t hg_selftest(hg_ctx* ctx, int32_t test, int64_t* tested);
 
 /* ----------------------------------------------------------------------------------------------
@@ -292,11 +304,24 @@ int hg_comm_init_all(hg_ctx* const* ctxs, int32_t n_ranks, hg_comm** out);
  * tiles to `root`, which assembles the full row-major RGBA32F image on its device.  Asynchronous on the contexts'
  * streams.  All ranks must have the same target size. */
 int hg_comm_gather(hg_comm* comm, int32_t root);
-/* On the process holding the root (after hg_comm_gather): the assembled image, width*height*4 floats. Blocks. */
+/* Wait until this process's ranks have finished the last gather (sends done; on the root, image assembled).  Like every
+ * wait of hg_comm it is bounded: RCCL errors (ncclCommGetAsyncError) and a deadline that starts once this process's own
+ * renders have retired end it with HG_E_COMM and abort the communicator (a dead or stalled peer never hangs the caller).
+ * A failed agreement (ranks with different target sizes or tilings) fails hg_comm_gather on every rank alike. */
+int hg_comm_synchronize(hg_comm* comm);
+/* On the process holding the root (after hg_comm_gather): the assembled image, width*height*4 floats. Blocks, with the
+ * deadline of hg_comm_synchronize. */
 int hg_comm_readback(hg_comm* comm, float* rgba, size_t n_floats);
+/* The deadline of every wait (default 120000 ms, or the environment variable HALOGEN_COMM_TIMEOUT_MS at init). */
+int hg_comm_set_timeout_ms(hg_comm* comm, int64_t timeout_ms);
 int hg_comm_transport(const hg_comm* comm);     /* HG_COMM_RCCL or HG_COMM_PEER */
 const char* hg_comm_last_error(const hg_comm* comm);
 void hg_comm_destroy(hg_comm* comm);
+/* Host twin of the root's assembly (no device work): slabs = [n_ranks][slab_tiles][64] RGBA32F tiles, slab r holding
+ * rank r's accumulated tiles in its local order (as hg_copy_tiles_device packs them); writes the row-major
+ * width*height*4 image.  Shares the tile -> rank / slot / pixel mapping with the device assembly (csrc/hg_tiling.h). */
+int hg_comm_assemble_host(const float* slabs, int64_t slab_tiles, int32_t width, int32_t height, int32_t n_ranks,
+                          float* rgba, size_t n_floats);
 
 /* ----------------------------------------------------------------------------------------------
  * Host-side data producers (the reference keeps these in C#: BVHGenerator.cs, RayTracingMesh.cs,

@@ -253,6 +253,16 @@ class HalogenRenderPass {
         return img;
     }
 
+    // Checkpoint / resume (not in the reference, whose resumable state is the accumulation RTHandle and the FrameCount
+    // field, RP:152,185,347): Restore(Readback(), getFrameCount()) on a new pass of the same width x height continues
+    // the progressive render bit-identically (hg_set_accumulation).
+    void Restore(const std::vector<float>& image, int32_t width, int32_t height, int32_t frame_count) {
+        OnCameraSetup(width, height);
+        check(hg_set_accumulation(ctx_, image.data(), image.size(), frame_count), "hg_set_accumulation");
+        FrameCount = frame_count;
+        AccumulationBufferDirty = false;
+    }
+
     hg_counters Counters() const {
         hg_counters c{};
         check(hg_get_counters(ctx_, &c), "hg_get_counters");

@@ -5,7 +5,8 @@ tiles with the frame-parallel split forced on (several waves per tile, colours b
 showed the round-1 zero-block observation), hg_comm_init_all joins them (contexts sharing a device take the
 in-process device-copy transport; RCCL refuses two ranks on one GPU), hg_comm_gather assembles the image on the
 root's device.  The merged image must be bit-equal to a 1-rank render and every pixel written (alpha == 1).
-A 1-rank communicator through hg_comm_init_rank exercises the RCCL transport's set-up and assembly on this GPU."""
+A 1-rank communicator through hg_comm_init_rank exercises the RCCL transport's set-up, agreement and assembly on this
+GPU; a 2-rank communicator whose peer never joins must fail within its deadline (SURVEY.md §5 failure detection)."""
 import numpy as np
 import pytest
 
@@ -71,11 +72,58 @@ def test_gpu_comm_rccl_single_rank(gpu):
         comm = abi.Comm.rank(ctx, 1, abi.comm_unique_id(), 0)
         assert comm.transport == abi.HG_COMM_RCCL
         comm.gather(0)
+        comm.synchronize()
         img = comm.readback(64, 64)
         assert_bitwise(img, ctx.readback(64, 64), "1-rank RCCL gather")
+        # the agreement all-reduce sees a context not tiled for this communicator: a loud error, not a hang
+        ctx.set_tiling(0, 2)
+        with pytest.raises(abi.HalogenError, match="tiled as 0/2"):
+            comm.gather(0)
+        ctx.set_tiling(0, 1)
+        ctx.render(frames, acc)
+        comm.gather(0)
+        assert_bitwise(comm.readback(64, 64), ctx.readback(64, 64), "1-rank RCCL gather after a refused one")
         comm.close()
     finally:
         ctx.close()
+
+
+_DEAD_PEER = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from halogen import abi
+ctx = abi.Context(0)
+ctx.resize(64, 64)
+ctx.set_tiling(0, 2)
+t0 = time.time()
+try:
+    abi.Comm.rank(ctx, 2, abi.comm_unique_id(), 0)  # rank 1 never joins
+    print("JOINED")
+except abi.HalogenError as e:
+    print("FAILED-LOUDLY %.1f %s" % (time.time() - t0, e))
+ctx.close()
+"""
+
+
+@pytest.mark.gpu
+def test_gpu_comm_dead_peer_fails_within_deadline(gpu, tmp_path):
+    """A 2-rank communicator whose second rank never joins: hg_comm_init_rank (non-blocking RCCL init polled with
+    ncclCommGetAsyncError) gives up at the deadline (HALOGEN_COMM_TIMEOUT_MS), aborts the communicator and returns
+    HG_E_COMM with text, instead of blocking forever.  Run in a child process so that a hang could not take the test
+    session with it."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    pkg = str(Path(__file__).resolve().parents[1] / "halogen-pathtracer_amd")
+    env = dict(os.environ, HALOGEN_COMM_TIMEOUT_MS="3000")
+    r = subprocess.run([sys.executable, "-c", _DEAD_PEER, pkg], env=env, capture_output=True, text=True, timeout=100)
+    out = r.stdout + r.stderr
+    assert "FAILED-LOUDLY" in r.stdout, out[-2000:]
+    secs = float(r.stdout.split("FAILED-LOUDLY")[1].split()[0])
+    assert 2.5 <= secs < 60, out[-2000:]
+    assert "communicator aborted" in r.stdout and "3000 ms" in r.stdout, out[-2000:]
 
 
 @pytest.mark.gpu

@@ -42,6 +42,9 @@ def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=Non
     img = np.full((H, W, 4), np.nan, np.float32)
     ctx.readback(W, H, img)
     cnt = ctx.counters()
+    if os.environ.get("HG_EXPECT_NO_EXEC_FALLBACK") == "1":  # tests/test_gpu_check_exec.py: an HG_CHECK_EXEC=1 build
+        assert ctx.selftest(abi.HG_SELFTEST_BUILD)[0] & abi.HG_BUILD_CHECK_EXEC, f"{abi.LIB_PATH} is not a check build"
+        assert cnt["exec_fallbacks"] == 0, f"leaf_dist ran under a partial EXEC {cnt['exec_fallbacks']} times"
     if own:
         ctx.close()
     return img, cnt

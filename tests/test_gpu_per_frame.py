@@ -1,0 +1,140 @@
+"""The drop-in's operating point and its checkpoint state, through the C-ABI.
+
+The reference dispatches HalogenCompute once per frame (RP:327, dispatch RP:406) and blends it into the accumulation
+target (RP:343-347); hg_render(n) runs n such frames in one launch.  A 1-frame launch takes its own path through the
+kernels (each pixel's one item blends straight into the accumulator, no frame-colour buffer, no blend pass; the tile
+order is re-sorted only every HG_ORDER_MIN_FRAMES frames), so it is checked bit for bit against the batched launch.
+
+Checkpoint/resume: the reference's resumable state is the accumulation target plus FrameCount (RP:152, 185, 347);
+hg_readback exports it and hg_set_accumulation restores it into a fresh context."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import cases
+import hg_oracle
+from halogen import abi, render_pass as rp, scenes
+from test_gpu_parity import assert_bitwise, gpu_render
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _full(cfg_name):
+    cfg = scenes.CONFIGS[cfg_name]
+    settings = scenes.settings_for(cfg)
+    s = rp.clamp_settings(settings)
+    packed = cases._scene(cfg.scene, 10)
+    cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
+    params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
+    return packed, params, cube
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dragon10_64x36", "glass_64x36", "c1_64", "c1_48_noacc", "c1_64_spp3"])
+def test_gpu_one_frame_launches_match_golden(gpu, name):
+    """frames x hg_render(1) (the reference's per-frame dispatches) equals the golden image and counters, and the
+    batched hg_render(frames), for the streaming (dragon, Cornell) and regenerating (glass) kernels, without
+    accumulation and with spp 3."""
+    meta = json.loads((GOLD / f"{name}.json").read_text())
+    packed, params, cube, frames, acc = cases.setup(name)
+    img, cnt = gpu_render(packed, params, frames, acc, cube, splits=[1] * frames)
+    assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name} as {frames} x render(1)")
+    for k, v in meta["counters"].items():
+        assert cnt[k] == v, (k, cnt[k], v)
+    assert cnt["launches"] == frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name", ["C3", "C5"])
+def test_gpu_one_frame_launches_match_batched_full_size(gpu, cfg_name):
+    """BASELINE's C3 (871k dragon, streaming kernel) and C5 (glass + cubemap, regenerating kernel) at 1920x1080:
+    64 x hg_render(1) from a cleared accumulator is bit-identical to one hg_render(64) over the whole image, and a
+    band of rows of it equals the live oracle."""
+    packed, params, cube = _full(cfg_name)
+    frames = 64
+    batched, bc = gpu_render(packed, params, frames, True, cube)
+    single, sc = gpu_render(packed, params, frames, True, cube, splits=[1] * frames)
+    assert_bitwise(single, batched, f"{cfg_name}: 64 x render(1) vs render(64)")
+    for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+        assert sc[k] == bc[k], (k, sc[k], bc[k])
+    W = int(params.screenParameters.x)
+    y0, y1 = 538, 540
+    ref, _ = hg_oracle.render(packed, params, 2, True, cubemap=cube, pix_range=(y0 * W, y1 * W))
+    two, _ = gpu_render(packed, params, 2, True, cube, splits=[1, 1])
+    assert_bitwise(two[y0:y1], ref[y0:y1], f"{cfg_name} rows {y0}-{y1}, 2 x render(1) vs oracle")
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_launch_sizes_with_tile_order(gpu):
+    """1-frame launches between multi-frame ones, with the cost order re-sorted only every 16 frames and a rank's share
+    of the tiles: the same image as one launch."""
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    for tiling in (None, (1, 3)):
+        ref, _ = gpu_render(packed, params, 40, True, cube, tiling=tiling)
+        img, _ = gpu_render(packed, params, 40, True, cube, tiling=tiling, splits=[1] * 17 + [5] + [1] * 18)
+        assert_bitwise(img, ref, f"mixed launches, tiling {tiling}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dragon10_64x36", "glass_64x36", "c1_64_spp3"])
+def test_gpu_checkpoint_resume_bit_identical(gpu, name):
+    """render(16) -> hg_readback -> a NEW context -> hg_set_accumulation(image, FrameCount 17) -> render(16) equals
+    render(32) bit for bit; also as one rank's share of a 3-way tiling."""
+    packed, params, cube, frames, acc = cases.setup(name)
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    for tiling in (None, (2, 3)):
+        ref, _ = gpu_render(packed, params, 32, True, cube, tiling=tiling)
+        first, _ = gpu_render(packed, params, 16, True, cube, tiling=tiling)
+        with abi.Context(0) as ctx:
+            ctx.upload_scene(packed)
+            if cube is not None:
+                ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+            ctx.resize(W, H)
+            if tiling:
+                ctx.set_tiling(*tiling)
+            ctx.set_params(params)  # frameCount 1: hg_set_accumulation below overrides it
+            ctx.set_accumulation(np.nan_to_num(first, nan=0.0), 17)
+            ctx.render(16, True)
+            img = np.full((H, W, 4), np.nan, np.float32)
+            ctx.readback(W, H, img)
+        assert_bitwise(img, ref, f"{name} resumed at frame 17, tiling {tiling}")
+
+
+@pytest.mark.gpu
+def test_gpu_render_pass_restore(gpu):
+    """HalogenRenderPass.restore(read_image(), getFrameCount()) on a new pass continues bit-identically."""
+    cfg = scenes.CONFIGS["C1"].resized(40, 32, 3)
+    scene = cfg.build_scene()
+    cam = cfg.camera()
+    a = rp.HalogenRenderPass(cfg.settings)
+    for _ in range(6):
+        a.Execute(scene, cam)
+    want = a.read_image()
+    b = rp.HalogenRenderPass(cfg.settings)
+    for _ in range(3):
+        b.Execute(scene, cam)
+    state = (b.read_image(), b.getFrameCount())
+    b.Dispose()
+    c = rp.HalogenRenderPass(cfg.settings)
+    c.restore(*state)
+    for _ in range(3):
+        c.Execute(scene, cam)
+    assert c.getFrameCount() == a.getFrameCount() == 7
+    assert_bitwise(c.read_image(), want, "render pass restore")
+    a.Dispose()
+    c.Dispose()
+
+
+@pytest.mark.gpu
+def test_gpu_set_accumulation_errors_are_loud(gpu):
+    packed, params, cube, frames, acc = cases.setup("c1_64")
+    with abi.Context(0) as ctx:
+        with pytest.raises(abi.HalogenError, match="hg_resize not called"):
+            ctx.set_accumulation(np.zeros((64, 64, 4), np.float32), 1)
+        ctx.resize(64, 64)
+        with pytest.raises(abi.HalogenError, match="too small"):
+            ctx.set_accumulation(np.zeros((32, 64, 4), np.float32), 1)
+        with pytest.raises(abi.HalogenError, match="frame_count"):
+            ctx.set_accumulation(np.zeros((64, 64, 4), np.float32), 0)
