@@ -91,32 +91,44 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
 
 def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_value: float) -> dict:
     """The drop-in's operating point: the reference dispatches HalogenCompute once per frame (RP:327, RP:406) and the
-    C# shim does hg_render(ctx, 1, 1) per Execute.  The same C3 step (`frames` progressive frames from a cleared
-    accumulator) is rendered as `frames` x hg_render(1) and compared bit for bit with one hg_render(frames); then timed
-    without a host copy (`reps` steps; device sync on both sides) and with the per-frame hg_readback of the 33 MB
-    image the C# pass does (HalogenRenderPass.cs Execute)."""
+    C# shim calls hg_render(ctx, 1, 1) per Execute.  The same C3 step (`frames` progressive frames from a cleared
+    accumulator) is rendered as `frames` x hg_render(1) and compared bit for bit with one hg_render(frames), then timed
+    (`reps` steps; device sync on both sides):
+      value       the library's default: consecutive calls are held and launched HG_OPT_COALESCE (32) frames at a time;
+      strict      HG_OPT_COALESCE 1: every call its own launch (traces of consecutive launches overlap on two streams);
+      with_readback  the C# pass's per-frame hg_readback of the 33 MB image after every call (which launches the held
+                  frame, so this is one launch per frame too)."""
     def fresh():
         ctx.clear_accumulation()
         ctx.set_params(params)
 
+    def timed(coalesce: int):
+        ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
+        ctx.reset_counters()
+        fresh()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for _ in range(frames):
+                ctx.render(1, True)
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        c = ctx.counters()
+        return dt, c
+
     fresh()
     ctx.render(frames, True)
     batched = ctx.readback(W, H)
-    fresh()
-    for _ in range(frames):
-        ctx.render(1, True)
-    single = ctx.readback(W, H)
-    identical = bool(np.array_equal(batched.view(np.uint32), single.view(np.uint32)))
-    ctx.reset_counters()
-    fresh()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    identical = {}
+    for coalesce in (1, 32):
+        ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
+        fresh()
         for _ in range(frames):
             ctx.render(1, True)
-    ctx.synchronize()
-    dt = time.perf_counter() - t0
-    c = ctx.counters()
+        identical[f"coalesce_{coalesce}"] = bool(np.array_equal(batched.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
+    paths = W * H * frames
+    dt, c = timed(32)
+    dt_s, c_s = timed(1)
     img = np.empty((H, W, 4), np.float32)
     fresh()
     ctx.synchronize()
@@ -125,11 +137,14 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         ctx.render(1, True)
         ctx.readback(W, H, img)
     dt_rb = time.perf_counter() - t1
-    paths = W * H * frames
+    ctx.set_option(abi.HG_OPT_COALESCE, 32)
     value = paths * reps / dt / 1e6
-    return {"workload": f"{frames} x hg_render(1) per step (RP:327 one dispatch per frame)", "value": value,
+    strict = paths * reps / dt_s / 1e6
+    return {"workload": f"{frames} x hg_render(1) per step (RP:327 one call per frame)", "value": value,
             "unit": "Mpaths/s", "steps": reps, "ms_per_frame": dt * 1e3 / (reps * frames),
-            "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1), "frac_of_batched": value / batched_value,
+            "launches_per_step": c["launches"] / reps, "frac_of_batched": value / batched_value,
+            "strict": {"value": strict, "ms_per_frame": dt_s * 1e3 / (reps * frames),
+                       "launches_per_step": c_s["launches"] / reps, "frac_of_batched": strict / batched_value},
             "with_readback": {"value": paths / dt_rb / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_rb * 1e3 / frames,
                               "readback_bytes_per_frame": W * H * 16},
             "bit_identical_to_batched": identical}
@@ -141,7 +156,7 @@ def library_sha256() -> str:
     return hashlib.sha256(abi.LIB_PATH.read_bytes()).hexdigest()
 
 
-def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str) -> dict:
+def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str, step_s: float = 0.0) -> dict:
     """The dominant kernel against what bounds it.  The trace kernel works on a cache-resident scene (C3: 90 MB,
     inside the 256 MiB Infinity Cache) and is bound by VALU issue and latency, not HBM: `frac` is its VALU issue rate
     (wave-level VALU instructions per launch, SQ_INSTS_VALU from the committed rocprofv3 pass of this workload and
@@ -171,6 +186,9 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "logical_bytes_per_launch": logical_per_launch,
             "logical_gbs": logical_per_launch / mean_launch_s / 1e9 if logical_per_launch and ok else None,
             "mean_launch_ms": mean_launch_s * 1e3, "kernel": kernel_symbol,
+            # launches of consecutive steps overlap (two trace streams): the step period is the throughput's clock
+            "step_period_ms": step_s * 1e3 if step_s else None,
+            "frac_per_step_period": valu / step_s / 1e9 / VALU_PEAK_GINST if valu and step_s else None,
             "counters_from": pmc.get("summary"),
             "counters_library_matches": (pmc.get("library_sha256") == lib_sha) if pmc.get("library_sha256") else None}
 
@@ -217,6 +235,8 @@ def main():
     ap.add_argument("--no-per-frame", action="store_true", help="skip the one-dispatch-per-frame leg")
     ap.add_argument("--per-frame-only", action="store_true",
                     help="profiling aid: only the per-frame leg's timed part (no headline line)")
+    ap.add_argument("--launch-frames", type=int, default=1, help="--per-frame-only: frames per hg_render call")
+    ap.add_argument("--coalesce", type=int, default=1, help="--per-frame-only: HG_OPT_COALESCE (1: every call launches)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
@@ -279,8 +299,10 @@ def main():
                                        "mega": abi.HG_KERNEL_MEGA,
                                        "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
                                        "pool": abi.HG_KERNEL_MEGA_POOL}[args.kernel])
-    if args.timing:
-        ctx.set_option(abi.HG_OPT_TIMING, 1)
+    # HIP events around every trace-kernel launch, on the trace stream it runs on (hg_counters.trace_ms): the roofline's
+    # launch duration.  (kernel_ms spans a launch from its trace's start to its blend's end; consecutive launches
+    # overlap on the two trace streams, so those spans overlap too.)
+    ctx.set_option(abi.HG_OPT_TIMING, 1)
     if args.refill:
         ctx.set_option(abi.HG_OPT_REFILL, args.refill)
     if args.block:
@@ -312,19 +334,20 @@ def main():
 
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
     if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step, then steps x frames x hg_render(1)
+        ctx.set_option(abi.HG_OPT_COALESCE, args.coalesce)
         ctx.render(frames_per_step, True)
         ctx.clear_accumulation()
         ctx.set_params(params)
         ctx.reset_counters()
         ctx.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps * frames_per_step):
-            ctx.render(1, True)
+        for _ in range(args.steps * frames_per_step // args.launch_frames):
+            ctx.render(args.launch_frames, True)
         ctx.synchronize()
         dt = time.perf_counter() - t0
         c = ctx.counters()
         print(json.dumps({"per_frame_only": True, "value": W * H * frames_per_step * args.steps / dt / 1e6,
-                          "unit": "Mpaths/s", "launches": c["launches"],
+                          "unit": "Mpaths/s", "launches": c["launches"], "ms_per_step": dt * 1e3 / args.steps,
                           "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1)}), flush=True)
         ctx.close()
         return
@@ -399,7 +422,8 @@ def main():
         if timed_img is not None:
             replay_identical = bool(np.array_equal(timed_img.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
     cnt = ctx.counters()
-    cnt["kernel_ms"], cnt["launches"] = timing["kernel_ms"], timing["launches"]
+    for k in ("kernel_ms", "launches", "trace_ms", "trace_launches"):
+        cnt[k] = timing[k]
     if dist is not None:
         import torch
 
@@ -419,7 +443,9 @@ def main():
     result = None
     if rank == 0:
         launches = max(cnt["launches"], 1)
-        mean_launch_s = cnt["kernel_ms"] / 1e3 / launches
+        # the trace kernel's own launch duration (events on its stream; what rocprofv3 --stats averages)
+        mean_launch_s = (cnt["trace_ms"] / cnt["trace_launches"] if cnt.get("trace_launches") else
+                         cnt["kernel_ms"] / launches) / 1e3
         counters_ok = not args.no_counters and cnt["paths"] > 0
         # §8(d)'s byte model: LOGICAL bytes per launch (every node / triangle / record read the algorithm makes,
         # whether L1/L2/Infinity Cache or HBM serves it) — a work measure, not a bound on this cache-resident kernel
@@ -435,7 +461,8 @@ def main():
                     pmc = t
             except Exception:
                 pmc = {}
-        roofline = roofline_of(pmc, mean_launch_s, logical_per_launch, kernel_symbol)
+        roofline = roofline_of(pmc, mean_launch_s, logical_per_launch, kernel_symbol,
+                               dt / max(args.steps, 1) if launches == args.steps else 0.0)
         result = {
             "metric": METRIC,
             "value": total_paths / dt / 1e6,

@@ -67,7 +67,7 @@ public static class HalogenNative
     public const int HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
                      HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-                     HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8;
+                     HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9;
     public const int HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2, HG_BUILD_CHECK_EXEC = 1;
     public const int HG_COMM_ID_BYTES = 128, HG_COMM_RCCL = 1, HG_COMM_PEER = 2;
 

@@ -15,7 +15,9 @@
 // kernel or copy on a stream the root's stream waits on: no host-visible buffer, no foreign stream.
 //
 // Failure behaviour (SURVEY.md §5 "failure detection"): nothing here waits without a deadline.
-//   - hg_comm_init_rank builds a NON-BLOCKING communicator and polls ncclCommGetAsyncError until it is ready;
+//   - hg_comm_init_rank runs ncclCommInitRank on a helper thread and waits for it with the deadline: RCCL's own
+//     "non-blocking" init (ncclConfig_t.blocking = 0) was measured to block in the calling thread while a peer is
+//     missing.  An init abandoned at the deadline is aborted by its thread if it ever completes;
 //   - every gather first agrees on the target size and tiling of all ranks (one 5-int ncclAllReduce, max of (v, -v)),
 //     so a mismatched rank fails the gather on EVERY rank with the same text instead of leaving its peers blocked in
 //     mismatched sends / receives; every ncclGroupStart is closed by its ncclGroupEnd on every path;
@@ -29,6 +31,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -96,11 +101,29 @@ int64_t env_timeout_ms() {
 
 using Clock = std::chrono::steady_clock;
 
+// HALOGEN_COMM_DEBUG=1: trace the communicator's waits on stderr (diagnostics of peer failures)
+bool comm_debug() {
+    static const bool on = [] {
+        const char* v = std::getenv("HALOGEN_COMM_DEBUG");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+#define HG_CDBG(...)                                     \
+    do {                                                 \
+        if (comm_debug()) {                              \
+            std::fprintf(stderr, "[hg_comm] " __VA_ARGS__); \
+            std::fflush(stderr);                         \
+        }                                                \
+    } while (0)
+
 // Abort every member communicator (RCCL's kernels of an aborted comm return) and make the comm unusable.
 void abort_all(hg_comm* m) {
     for (auto& mb : m->members)
         if (mb.nccl) {
-            (void)ncclCommAbort(mb.nccl);
+            HG_CDBG("ncclCommAbort rank %d\n", mb.rank);
+            const ncclResult_t r = ncclCommAbort(mb.nccl);
+            HG_CDBG("ncclCommAbort rank %d -> %s\n", mb.rank, ncclGetErrorString(r));
             mb.nccl = nullptr;
         }
     m->aborted = true;
@@ -126,6 +149,7 @@ ncclResult_t async_state(hg_comm* m, int32_t* bad_rank) {
 // Wait until every member communicator has finished its pending (non-blocking) operation: init, or a group call.
 int wait_comms_ready(hg_comm* m, const char* what) {
     const auto deadline = Clock::now() + std::chrono::milliseconds(m->timeout_ms);
+    HG_CDBG("%s: waiting up to %lld ms\n", what, (long long)m->timeout_ms);
     for (;;) {
         int32_t bad = -1;
         const ncclResult_t st = async_state(m, &bad);
@@ -340,18 +364,55 @@ int hg_comm_init_rank(hg_ctx* ctx, int32_t n_ranks, const uint8_t id[HG_COMM_ID_
         hg_comm_destroy(m);
         return rc;
     }
-    // non-blocking: the call returns while the ranks bootstrap; wait_comms_ready bounds the wait for the peers
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
-    const ncclResult_t r = ncclCommInitRankConfig(&mb.nccl, n_ranks, u, rank, &cfg);
-    int rc = HG_OK;
-    if (r != ncclSuccess && r != ncclInProgress) {
-        rc = cfail(m, HG_E_COMM, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(r));
-        if (mb.nccl) (void)ncclCommAbort(mb.nccl);
-        mb.nccl = nullptr;
-    } else {
-        rc = wait_comms_ready(m, "ncclCommInitRankConfig");
+    // The init blocks until every rank has joined: a helper thread makes the call and this one waits with the
+    // deadline.  At the deadline the job is abandoned; its thread aborts the communicator if the init ever returns.
+    struct InitJob {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = ncclSuccess;
+    };
+    auto job = std::make_shared<InitJob>();
+    const int dev = ctx->device;
+    HG_CDBG("ncclCommInitRank rank %d of %d on a helper thread, deadline %lld ms\n", rank, n_ranks,
+            (long long)m->timeout_ms);
+    try {
+        std::thread([job, n_ranks, u, rank, dev]() {
+            ncclComm_t cm = nullptr;
+            ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclCommInitRank(&cm, n_ranks, u, rank)
+                                                             : ncclUnhandledCudaError;
+            std::lock_guard<std::mutex> lk(job->mu);
+            if (job->abandoned) {
+                if (cm) (void)ncclCommAbort(cm);
+                return;
+            }
+            job->comm = cm;
+            job->r = r;
+            job->done = true;
+            job->cv.notify_all();
+        }).detach();
+    } catch (const std::exception& ex) {
+        ctx->err = std::string("hg_comm_init_rank: cannot start the init thread: ") + ex.what();
+        hg_comm_destroy(m);
+        return HG_E_COMM;
     }
+    int rc = HG_OK;
+    {
+        std::unique_lock<std::mutex> lk(job->mu);
+        if (!job->cv.wait_for(lk, std::chrono::milliseconds(m->timeout_ms), [&] { return job->done; })) {
+            job->abandoned = true;
+            rc = cfail(m, HG_E_COMM, "ncclCommInitRank: rank %d of %d: the other ranks did not all join within %lld ms "
+                                     "(a peer missing or failed?); init abandoned", rank, n_ranks,
+                       (long long)m->timeout_ms);
+        } else if (job->r != ncclSuccess) {
+            rc = cfail(m, HG_E_COMM, "ncclCommInitRank failed: %s", ncclGetErrorString(job->r));
+            if (job->comm) (void)ncclCommAbort(job->comm);
+        } else {
+            mb.nccl = job->comm;
+        }
+    }
+    HG_CDBG("ncclCommInitRank -> %d\n", rc);
     if (rc != HG_OK) {
         ctx->err = m->err;
         hg_comm_destroy(m);
@@ -419,6 +480,8 @@ int hg_comm_gather(hg_comm* m, int32_t root) {
     if (!m) return HG_E_INVALID;
     if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
     if (root < 0 || root >= m->n_ranks) return cfail(m, HG_E_INVALID, "root %d out of range", root);
+    for (auto& mb : m->members)  // held hg_render frames are launched before the accumulators are read
+        if (hg_ctx_flush(mb.ctx) != HG_OK) return cfail(m, HG_E_HIP, "rank %d: %s", mb.rank, mb.ctx->err.c_str());
     int32_t W = m->members.front().ctx->W, H = m->members.front().ctx->H;
     if (m->transport == HG_COMM_RCCL) {
         if (int rc = agree_on_target(m, W, H)) return rc;

@@ -44,12 +44,30 @@ struct hg_ctx {
     DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
     DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
     DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
-    DevBuf frame_color;          // frame-parallel split: per-frame colours of this launch chunk
     DevBuf pool;                 // path-pool kernel: per-wave path slots
-    DevBuf tile_cost, tile_order;  // cost-ordered dispatch: per local tile, wave-clock cost / dispatch order
-    bool tile_cost_valid = false;  // tile_cost holds the costs recorded since the last sort, for this tiling
-    bool tile_order_valid = false;  // tile_order holds a sorted order for this tiling
-    int64_t frames_since_order = 0;  // frames whose wave times tile_cost has accumulated since the last sort
+    // Trace pipeline (hg_render): the regenerating / streaming kernels trace each launch chunk on one of HG_TRACE_LANES
+    // side streams, in turn, into that stream's own frame-colour buffer; the chunk's in-order blend into the accumulator
+    // runs on `stream`.  So a chunk's tail overlaps the next chunk's trace, and everything else on `stream` (readback,
+    // clear, gather) stays ordered after the blends.  Per trace stream: its buffers and the events that order them.
+    struct TraceLane {
+        hipStream_t stream = nullptr;
+        hipEvent_t traced = nullptr;   // after this stream's last trace (the blend on `stream` waits for it)
+        hipEvent_t blended = nullptr;  // after the blend of this stream's last chunk (its buffers are free again)
+        bool blend_pending = false;    // `blended` was recorded and the next trace here must wait for it
+        DevBuf frame_color;            // this chunk's per-frame colours ([slot][frame], fc_index)
+        DevBuf spill;                  // traversal stack entries beyond the LDS part, one column per thread
+        // Cost order: this stream's traces add their wave times to tile_cost and its sorts read and clear them, all in
+        // this stream's order.  (One buffer shared by both streams let a sort read costs that the other stream's trace
+        // was still adding to: the counting sort's two passes then disagreed and wrote out of range.)
+        DevBuf tile_cost;              // per local tile, wave-clock cost since this stream's last sort
+        DevBuf tile_order;             // the cost order this stream's launches read
+        DevBuf queue;                  // kQueue launches: the 8 unit heads (zeroed per launch)
+        bool tile_cost_valid = false;  // tile_cost holds costs for this tiling
+        bool tile_order_valid = false;
+        int64_t frames_since_order = 0;  // frames traced on this stream since its last sort
+    };
+    TraceLane lanes[HG_TRACE_LANES];
+    int next_lane = 0;
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;
@@ -65,4 +83,13 @@ struct hg_ctx {
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
     int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
     int32_t tile_order_on = HG_TILE_ORDER;  // HG_OPT_TILE_ORDER
+    // Render coalescing (HG_OPT_COALESCE): hg_render is asynchronous, so consecutive calls with the same parameters are
+    // held and launched as one multi-frame launch once `coalesce` frames are pending, or as soon as anything reads or
+    // changes the context's state (every other entry point flushes first: hg_ctx_flush).  Same frames, same order,
+    // same image; 1 = every call launches at once.
+    int32_t coalesce = HG_COALESCE;
+    int32_t pending_frames = 0, pending_acc = 0;
 };
+
+// Launch the held frames of a context, if any (hg_runtime.hip; every entry point but hg_render calls it first)
+int hg_ctx_flush(hg_ctx* c);

@@ -221,12 +221,17 @@ __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
 }
 
 // Frame colour of launch frame f (0 .. n_frames-1) for accumulator slot `slot` (hg_blend_frames reads the same layout)
-__device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f, size_t slot) {
+__device__ __forceinline__ size_t fc_slot_frame(size_t slot, uint32_t f, size_t n_slots, uint32_t n_frames) {
 #if HG_FC_SLOT_MAJOR
-    return slot * size_t(uint32_t(kp.n_frames)) + f;
+    (void)n_slots;
+    return slot * size_t(n_frames) + f;
 #else
-    return size_t(f) * (size_t(uint32_t(kp.n_local_tiles)) * 64u) + slot;
+    (void)n_frames;
+    return size_t(f) * n_slots + slot;
 #endif
+}
+__device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f, size_t slot) {
+    return fc_slot_frame(slot, f, size_t(uint32_t(kp.n_local_tiles)) * 64u, uint32_t(kp.n_frames));
 }
 
 // Triangle ti's Moller-Trumbore operands from the three SoA streams: a = (v0, e1.x), b = (e1.yz, e2.xy), cz = e2.z.

@@ -146,11 +146,22 @@
 // reserve; 0 keeps its mesh records in global memory
 #define HG_REGEN_LDS_BUDGET 6144
 #endif
-#ifndef HG_STREAM_ITEMS
-#define HG_STREAM_ITEMS 1  // streaming kernel: lanes take (pixel, frame) items of the wave's tile (frame colours blended after)
-#endif
+// (HG_STREAM_ITEMS, lanes owning pixels instead of taking (pixel, frame) items, is gone: the streaming kernel always takes
+// items and stores frame colours; hg_mega.hip)
 #ifndef HG_FC_SLOT_MAJOR
 #define HG_FC_SLOT_MAJOR 1  // frame colours stored [slot][frame] (a pixel's frames contiguous) instead of [frame][slot]
+#endif
+#ifndef HG_DIAG_NO_FC
+#define HG_DIAG_NO_FC 0  // analysis builds: the streaming kernel skips its frame-colour stores (wrong images; WRITE_SIZE split)
+#endif
+#ifndef HG_COALESCE
+#define HG_COALESCE 32  // default HG_OPT_COALESCE: frames of consecutive hg_render calls held for one launch
+#endif
+#ifndef HG_TRACE_LANES
+#define HG_TRACE_LANES 2  // trace streams of the render pipeline (hg_ctx.h): chunks traced in turn on them, blended in order
+#endif
+#ifndef HG_QUEUE_MAX_FRAMES
+#define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif
 #ifndef HG_ITEMS_PIXEL_MAJOR
 #define HG_ITEMS_PIXEL_MAJOR 1  // items k -> (pixel k / frames, frame k % frames): a wave's lanes trace one pixel's frames
@@ -216,6 +227,10 @@ struct HgKernelParams {
     // gives the same image: tiles are independent and each tile's frames keep their order.
     unsigned long long* __restrict__ tile_cost;  // s_memtime cycles per tile
     const uint32_t* __restrict__ tile_order;
+    // HG_STREAM_QUEUE: 8 unit heads (one per XCD, 128 B apart: queue[32 h]), zeroed before each streaming launch, and
+    // the number of persistent waves (one per resident wave slot of the GPU)
+    uint32_t* __restrict__ queue;
+    uint32_t resident_waves;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane

@@ -137,10 +137,15 @@ __device__ __forceinline__ void tile_cost_begin(const HgKernelParams& kp, uint32
         hg_wave_t0[threadIdx.x >> 6] = wave_clock();
     }
 }
+// a global-memory atomic add through a pointer kept in LDS (a generic pointer would compile to a FLAT atomic)
+__device__ __forceinline__ void cost_add(unsigned long long* p, uint64_t v) {
+    typedef __attribute__((address_space(1))) unsigned long long* gptr;
+    __hip_atomic_fetch_add((gptr)(uintptr_t)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void record_tile_cost(uint32_t lane) {
     if (lane != 0) return;
     unsigned long long* const p = hg_wave_cost[threadIdx.x >> 6];
-    if (p) atomicAdd(p, (unsigned long long)(wave_clock() - hg_wave_t0[threadIdx.x >> 6]));
+    if (p) cost_add(p, wave_clock() - hg_wave_t0[threadIdx.x >> 6]);
 }
 
 // RayColor / SamplesPerPixel (:1060); x / 1 == x exactly (NaN and signed zeros included), so spp 1 skips the divisions
@@ -162,6 +167,11 @@ struct TileItems {
 #if HG_ITEMS_PIXEL_MAJOR
     uint32_t nf;  // frames of the chunk
 #endif
+    __device__ TileItems() : tx0(0), ty0(0), tw(0), nv(0), n_items(0), f_begin(0) {  // unused (kQueue kernels)
+#if HG_ITEMS_PIXEL_MAJOR
+        nf = 1u;
+#endif
+    }
     __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe, uint32_t lane) {
         const int g = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
         tx0 = uint32_t(g % kp.tiles_x) * HG_TILE;
@@ -219,7 +229,8 @@ struct TileItems {
     }
 };
 
-// One workgroup of 1024 threads: tile_order = the local tiles by descending cost, STABLE (equal buckets keep
+// One workgroup of 1024 threads: tile_order = the local tiles by descending cost, STABLE (the costs must not change
+// during the sort: the runtime sorts a trace stream's own costs on that stream, hg_ctx.h TraceLane) (equal buckets keep
 // tile-index order, so the dispatch order of a launch is a deterministic function of the recorded costs), then the
 // costs are cleared for the next launch.  Counting sort over 1024 linear cost buckets (bucket 0 = most expensive):
 //   1. per-bucket counts over all tiles, exclusive prefix = each bucket's start;
@@ -247,7 +258,7 @@ __global__ __launch_bounds__(1024) void hg_order_tiles(unsigned long long* __res
         constexpr uint32_t B = HG_ORDER_BUCKETS;
         static_assert(B >= 1 && B <= 1024, "order buckets");
         const unsigned long long q = top / B + 1u;  // c / q < B for every c <= top
-        return B - 1u - uint32_t(c / q);
+        return B - 1u - uint32_t((c < top ? c : top) / q);  // (the clamp only guards: costs must not change meanwhile)
     };
     for (uint32_t i = t; i < n; i += 1024) atomicAdd(&start[bucket(cost[i])], 1u);
     __syncthreads();
@@ -283,7 +294,8 @@ __global__ __launch_bounds__(1024) void hg_order_tiles(unsigned long long* __res
         }
         __syncthreads();
         if (valid) {
-            order[start[b] + wcount[wave][b] + rank] = i;
+            const uint32_t pos = start[b] + wcount[wave][b] + rank;
+            if (pos < n) order[pos] = i;  // always true while the costs hold still during the sort (the caller's duty)
             cost[i] = 0;
         }
         __syncthreads();
@@ -406,7 +418,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
-                    if (split > 1u || (HG_REGEN_ITEMS && kp.n_frames > 1)) {  // colour, blended later in frame order
+                    if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
                         kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
                             make_float4(color.x, color.y, color.z, 1.0f);
                     } else {
@@ -559,9 +571,37 @@ __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ a
 }
 #endif
 
+// The blend of a launch of few frames (at most HG_QUEUE_MAX_FRAMES): one thread per slot, no LDS, 64-thread groups and
+// few registers.  A 1-frame launch's blend runs while the next launch's persistent trace waves hold the CUs' wave slots
+// and most of their LDS: this one fits beside them (the LDS-staged hg_blend_frames_sm, 36 KB per group, waited for
+// the trace to wind down: 0.7 ms per 1-frame blend on C3).  Same operations in the same order.
+__global__ __launch_bounds__(64) void hg_blend_frames_lean(float4* __restrict__ acc, const float4* __restrict__ colors,
+                                                           uint32_t n_slots, int32_t n_frames, int32_t first_frame,
+                                                           int32_t accumulate) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n_slots) return;
+    float4 a = acc[i];
+    for (int32_t f = 0; f < n_frames; ++f) {
+        const float4 c = colors[fc_slot_frame(i, uint32_t(f), n_slots, uint32_t(n_frames))];
+        if (accumulate) {
+            const float w = rcp_exact(float(uint32_t(first_frame + f)));
+            const float k = 1.0f - w;
+            a = make_float4(a.x * k + c.x * w, a.y * k + c.y * w, a.z * k + c.z * w, a.w * k + 1.0f * w);
+        } else {
+            a = make_float4(c.x, c.y, c.z, 1.0f);
+        }
+    }
+    acc[i] = a;
+}
+
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) {
     const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
     if (n_slots == 0) return hipSuccess;
+    if (kp.n_frames <= HG_QUEUE_MAX_FRAMES) {
+        hipLaunchKernelGGL(hg_blend_frames_lean, dim3((n_slots + 63) / 64), dim3(64), 0, stream, kp.acc, kp.frame_color,
+                           n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+        return hipGetLastError();
+    }
 #if HG_FC_SLOT_MAJOR
     hipLaunchKernelGGL(hg_blend_frames_sm, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc,
                        kp.frame_color, n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
@@ -597,23 +637,183 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp_in, int block, bool cou
     return hipGetLastError();
 }
 
+// Persistent streaming waves over a work queue (kQueue: launches of at most HG_QUEUE_MAX_FRAMES frames, e.g. the
+// reference's one dispatch per frame, RP:327).  The launch has one wave per resident wave slot
+// (kp.resident_waves, at most one per unit); each wave pulls (tile, frame chunk) units from the queue and hands their
+// (pixel, frame) items to its lanes in order (pixel-major, as TileItems).  A lane that finishes a frame takes the
+// wave's next item in place; a lane that finds the current unit spent idles until the top of the wave's loop, where
+// the wave pulls the next unit for its idle lanes, while the lanes still on the old unit's items carry on.  So a lane
+// idles only between a unit's end and the next loop top, and at the very end of the queue, not until its tile's
+// slowest path is done.  Without it a 1-frame launch (one item per pixel) kept each wave's 64 lanes waiting for its
+// tile's slowest path: 899 -> 1,383 Mpaths/s on C3 as 1-frame launches.  With 64-frame launches the per-tile waves win
+// (one tile's 4,096 items keep the lanes busy anyway; the queue's per-take LDS reads cost C3 2.6 %, C2 6.6 %).  The
+// queue is 8 heads, one per XCD
+// (workgroups are placed on XCD blockIdx mod 8): head h hands out units h, h + 8, h + 16, ... in the cost order
+// (wave_unit), and a wave whose head is dry steals from the others.  Which wave traces an item changes nothing: every
+// item runs with the inputs the reference's dispatch of that frame gives its pixel, and writes its own colour slot.
+// LDS words read / written by different lanes of the wave: relaxed workgroup-scope atomics on the __shared__ object
+// itself compile to plain ds_read / ds_write that the compiler may not cache in registers (a volatile access through
+// a cast pointer became a FLAT access with a 64-bit generic address and cost the kernel 60 B of scratch)
+__device__ __forceinline__ uint32_t lds_get(uint32_t& x) {
+    return __hip_atomic_load(&x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_put(uint32_t& x, uint32_t v) {
+    __hip_atomic_store(&x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr uint32_t kFreshLane = 0xFFFFFFFFu;  // `bounce` of a lane that has no path yet (it takes its item when shading)
+// The wave's two current units (double-buffered), in LDS (one wave per workgroup).  Item numbers (hg_next_item) run on
+// across units: unit hg_q_cur covers [base, end), the other one the numbers after it, so a lane whose take runs past
+// the first unit's items gets the second's at once; the loop top refills the spent unit.
+struct QueueUnit {
+    uint32_t base, end;                            // the wave's item numbers [base, end) are this unit's items
+    uint32_t tile, tx0, ty0, tw, nv, f_begin, nf;  // its tile (local index, origin, width, valid pixels), frames
+};
+__shared__ QueueUnit hg_qu[2];
+__shared__ uint32_t hg_q_cur;  // the unit whose items come first
+__shared__ uint32_t hg_q_dry;  // the queue has no unit left
+__shared__ uint32_t hg_q_empty;  // the queue has no unit left and both units are spent (the wave's lanes retire)
+
+// Pull the next unit of the queue into hg_qu[slot], its items numbered from `base` (one lane).  When the queue is dry
+// the unit is empty (end = base) and hg_q_dry is set.  Attributes the wave clock since the previous pull to the
+// previous unit's tile cost (the cost order of the next launches).
+__device__ __forceinline__ void queue_pull(const HgKernelParams& kp, uint32_t n_units, uint32_t split, uint32_t slot,
+                                           uint32_t base) {
+    const uint32_t x = blockIdx.x & 7u;
+    uint32_t u = n_units;
+    for (uint32_t t = 0; t < 8u && u >= n_units; ++t) {  // own XCD's head first, then steal
+        const uint32_t h = (x + t) & 7u;
+        if (h >= n_units) continue;
+        const uint32_t j = atomicAdd(kp.queue + 32u * h, 1u);
+        if (uint64_t(h) + 8ull * j < n_units) u = h + 8u * j;
+    }
+    QueueUnit& q = hg_qu[slot];
+    lds_put(q.base, base);
+    if (u >= n_units) {
+        lds_put(q.end, base);
+        lds_put(hg_q_dry, 1u);
+        return;  // the last unit's cost is recorded at the wave's end (record_tile_cost)
+    }
+    int tile;
+    uint32_t chunk;
+    wave_unit(kp, u, uint32_t(kp.n_local_tiles), split, tile, chunk);
+    const uint32_t fb = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
+    const uint32_t fe = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
+    const uint32_t g = uint32_t(kp.rank) + uint32_t(tile) * uint32_t(kp.n_ranks);
+    const uint32_t ty = g / uint32_t(kp.tiles_x);
+    const uint32_t tx0 = (g - ty * uint32_t(kp.tiles_x)) * HG_TILE, ty0 = ty * HG_TILE;
+    const uint32_t tw = min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0));
+    const uint32_t th = min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0));
+    const uint64_t now = wave_clock();
+    unsigned long long* const prev = hg_wave_cost[threadIdx.x >> 6];
+    if (prev) cost_add(prev, now - hg_wave_t0[threadIdx.x >> 6]);
+    hg_wave_cost[threadIdx.x >> 6] = kp.tile_cost ? kp.tile_cost + tile : nullptr;
+    hg_wave_t0[threadIdx.x >> 6] = now;
+    lds_put(q.tile, uint32_t(tile));
+    lds_put(q.tx0, tx0);
+    lds_put(q.ty0, ty0);
+    lds_put(q.tw, tw);
+    lds_put(q.nv, tw * th);
+    lds_put(q.f_begin, fb);
+    lds_put(q.nf, fe > fb ? fe - fb : 1u);
+    lds_put(q.end, base + tw * th * (fe - fb));
+}
+
+// Loop top (lane 0, the whole wave converged): keep both units filled.  Returns true when no item is left anywhere.
+__device__ __forceinline__ bool queue_refill(const HgKernelParams& kp, uint32_t n_units, uint32_t split) {
+    const uint32_t cnt = lds_get(hg_next_item);
+    uint32_t a = lds_get(hg_q_cur);
+    if (cnt >= lds_get(hg_qu[a].end) && !lds_get(hg_q_dry)) {  // the first unit is spent
+        const uint32_t b = a ^ 1u, b_end = lds_get(hg_qu[b].end);
+        if (cnt < b_end) {  // the second one is in use: it comes first now, the spent one is refilled after it
+            lds_put(hg_q_cur, b);
+            queue_pull(kp, n_units, split, a, b_end);
+            a = b;
+        } else {  // both spent (numbers taken by lanes that found them so are skipped): two new units
+            queue_pull(kp, n_units, split, a, cnt);
+            queue_pull(kp, n_units, split, b, lds_get(hg_qu[a].end));
+        }
+    }
+    return lds_get(hg_q_dry) && cnt >= lds_get(hg_qu[a ^ 1u].end) && cnt >= lds_get(hg_qu[a].end);
+}
+
+// Item number k of the wave, if one of the two current units holds it: its accumulator slot, frame and pixel
+// (pixel-major, as TileItems::get).  Called by the lanes that took k.
+__device__ __forceinline__ bool queue_item(uint32_t k, uint32_t& slot, uint32_t& frame, uint32_t& px, uint32_t& py) {
+    const uint32_t a = __builtin_amdgcn_readfirstlane(lds_get(hg_q_cur));
+    const uint32_t a_end = __builtin_amdgcn_readfirstlane(lds_get(hg_qu[a].end));
+    const uint32_t b_end = __builtin_amdgcn_readfirstlane(lds_get(hg_qu[a ^ 1u].end));
+    if (k >= b_end && k >= a_end) return false;
+    QueueUnit& q = hg_qu[k < a_end ? a : a ^ 1u];
+    const uint32_t base = lds_get(q.base);
+    if (k < base) return false;  // (never: numbers below the first unit were all handed out before it)
+    const uint32_t kk = k - base, nf = lds_get(q.nf), nv = lds_get(q.nv), tw = lds_get(q.tw);
+    uint32_t i, f;
+    if ((nf & (nf - 1u)) == 0u) {
+        const uint32_t lg = uint32_t(__builtin_ctz(nf));
+        i = kk >> lg;
+        f = kk & (nf - 1u);
+    } else {
+        i = kk / nf;
+        f = kk - i * nf;
+    }
+    const uint32_t pix = nv == 64u ? i : (i % tw) + 8u * (i / tw);
+    slot = lds_get(q.tile) * 64u + pix;
+    frame = lds_get(q.f_begin) + f;
+    px = lds_get(q.tx0) + (pix & 7u);
+    py = lds_get(q.ty0) + (pix >> 3);
+    return true;
+}
+
+// The lanes calling it (the active lanes) take the wave's next item numbers in lane order (one LDS atomic)
+__device__ __forceinline__ uint32_t queue_take() {
+    const uint64_t m = __builtin_amdgcn_read_exec();
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+    uint32_t b0 = 0;
+    if (rank == 0u) b0 = atomicAdd(&hg_next_item, uint32_t(__builtin_popcountll(m)));
+    return __builtin_amdgcn_readfirstlane(b0) + rank;
+}
+
+// The image pixel of accumulator slot `slot` (local tile slot / 64, pixel slot % 64)
+__device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t slot, uint32_t& x, uint32_t& y) {
+    const uint32_t g = uint32_t(kp.rank) + (slot >> 6) * uint32_t(kp.n_ranks);
+    const uint32_t ty = g / uint32_t(kp.tiles_x);
+    x = (g - ty * uint32_t(kp.tiles_x)) * HG_TILE + (slot & 7u);
+    y = ty * HG_TILE + ((slot >> 3) & 7u);
+}
+
 // Streaming variant (HG_KERNEL_MEGA_STREAM): the regenerating kernel with a resumable traversal.  Lanes advance
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
-template <bool kCounters, bool kMeshLds>
+// Every frame's colour goes to frame_color (item scheduling), blended in frame order by hg_blend_frames.  kQueue: the
+// persistent work-queue form above (launches of few frames).
+template <bool kCounters, bool kMeshLds, bool kQueue>
 __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
-    // one wave per workgroup (launched with 64 threads): wave = workgroup
-    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
-    int local_tile;
-    uint32_t chunk;
-    wave_unit(kp, gw, nlt, split, local_tile, chunk);
-    tile_cost_begin(kp, lane, local_tile, chunk < split);
-    const uint32_t f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
-    const uint32_t f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
+    const uint32_t n_units = nlt * split;  // kQueue: (tile, frame chunk) units of the queue
+    int local_tile = 0;
+    uint32_t chunk = 0, f_begin = 0, f_end = 0;
+    if constexpr (kQueue) {
+        if (lane == 0) {
+            lds_put(hg_next_item, 0u);
+            for (uint32_t u = 0; u < 2u; ++u) {
+                lds_put(hg_qu[u].base, 0u);
+                lds_put(hg_qu[u].end, 0u);
+            }
+            lds_put(hg_q_cur, 0u);
+            lds_put(hg_q_dry, 0u);
+            hg_wave_cost[threadIdx.x >> 6] = nullptr;
+        }
+    } else {
+        // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
+        // one wave per workgroup (launched with 64 threads): wave = workgroup
+        const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
+        wave_unit(kp, gw, nlt, split, local_tile, chunk);
+        tile_cost_begin(kp, lane, local_tile, chunk < split);
+        f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
+        f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
+    }
     const RowStack<HG_STREAM_LDS_STACK, kRowStack> stk{lane, kp.spill + blockIdx.x * 64u + lane, kp.spill_stride};
     const RowVec3<kRowThr> s_thr{lane};
     const RowVec3<kRowCol> s_col{lane};
@@ -632,14 +832,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         wave_lds_sync();
     }
 #endif
-    bool work;
-    uint32_t px, py;
-    {
-        const int gtile = kp.rank + local_tile * kp.n_ranks;
-        px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
-        py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
-        work = chunk < split && px < kp.Wu && py < kp.Hu && f_end > f_begin;
-    }
+    bool work = false;
+    uint32_t px = 0u, py = 0u;
     Counters c{0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t paths = 0;
     uint32_t fs = f_begin << 16;  // frame index << 16 | sample index
@@ -650,34 +844,50 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     float acc_rough = 0.0f;
     Trav tv;
     tv.mi = nm;
-#if HG_STREAM_ITEMS
-    const TileItems items(kp, local_tile, chunk < split, f_begin, f_end, lane);
-    uint32_t pix = lane;  // the item's pixel within the tile (x + 8 y)
-    if (lane < items.n_items) {  // item `lane`
-        uint32_t f;
-        items.get(lane, pix, f);
-        px = items.tx0 + (pix & 7u);
-        py = items.ty0 + (pix >> 3);
-        fs = f << 16;
-        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
-    }
-    work = lane < items.n_items;
-#else
-    const uint32_t pix = lane;
-#endif
-    if (work) {
-        ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
-        paths++;
-        s_thr.set(mk(1, 1, 1));
-        s_col.set(mk(0, 0, 0));
-        s_sum.set(mk(0, 0, 0));
-        trav_begin<kMeshLds>(kp, ray, tv, c);
+    uint32_t slot = 0;  // kQueue: the lane's item's accumulator slot (local tile * 64 + pixel)
+    bool dry = false;   // kQueue, wave-uniform: the queue has no unit left
+    uint32_t pix = lane;  // otherwise: the item's pixel within the wave's tile (x + 8 y)
+    const TileItems items = kQueue ? TileItems() : TileItems(kp, local_tile, chunk < split, f_begin, f_end, lane);
+    if constexpr (kQueue) {
+        wave_lds_sync();  // hg_q / hg_next_item initialised (lane 0); every lane takes its first item in the loop
+    } else {
+        if (lane < items.n_items) {  // item `lane`
+            uint32_t f;
+            items.get(lane, pix, f);
+            px = items.tx0 + (pix & 7u);
+            py = items.ty0 + (pix >> 3);
+            fs = f << 16;
+            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
+        }
+        work = lane < items.n_items;
+        if (work) {
+            ray = camera_ray(kp, smp, (float(px) / kp.W) * 2.0f - 1.0f, (float(py) / kp.H) * 2.0f - 1.0f);  // :1023-1033
+            paths++;
+            s_thr.set(mk(1, 1, 1));
+            s_col.set(mk(0, 0, 0));
+            s_sum.set(mk(0, 0, 0));
+            trav_begin<kMeshLds>(kp, ray, tv, c);
+        }
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
 #if HG_SHADE_PRIO >= 2
     __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);  // traversal waits on memory: its waves issue first
 #endif
-    while (__any(work)) {
+    for (;;) {
+        // ---- kQueue: the wave refills a spent unit, and idle lanes (the wave's start; lanes whose take found both
+        // units spent) become fresh: they take their item in the shading pass below
+        if (kQueue && !dry) {
+            wave_lds_sync();
+            if (lane == 0u) lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
+            wave_lds_sync();
+            dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
+            if (!work && !dry) {
+                work = true;
+                bounce = kFreshLane;
+                tv.mi = nm;
+            }
+        }
+        if (!__any(work)) break;
         // ---- traversal rounds until few lanes are left traversing
         if (kCounters) cyc_trav -= wave_clock();
         for (;;) {
@@ -708,12 +918,14 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #if HG_PHASE_DETAIL == 1
             uint64_t tp = kCounters ? wave_clock() : 0;
 #endif
+            const bool fresh = kQueue && bounce == kFreshLane;  // no path yet: straight to the take below
+            bool alive = false;
+            f3 thr = s_thr.get(), col = s_col.get();
+            if (!fresh) {
             const Hit hit = trav_hit<kMeshLds>(kp, ray, tv);
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 11, tp);
 #endif
-            bool alive = false;
-            f3 thr = s_thr.get(), col = s_col.get();
             if (hit.t < kp.far_) {  // :898-936
                 c.hits++;
                 const Mat mt = load_mat(kp, hit.mat);
@@ -737,6 +949,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
             }
+            }
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 12, tp);
 #endif
@@ -746,61 +959,49 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 const bool one_sample = kp.spp == 1;
                 f3 sum = one_sample ? col : s_sum.get() + col;
                 ++fs;
-                bool next = (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
+                bool next = !fresh && (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
-                    const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
-                    // A multi-frame launch stores this frame's colour, blended later in frame order (hg_blend_frames);
-                    // a 1-frame launch (the reference's one dispatch per frame, RP:327) has one item per pixel and
-                    // blends it straight into the accumulator: the same operations, no colour buffer, no blend pass.
-                    if (split > 1u || (HG_STREAM_ITEMS && kp.n_frames > 1)) {
-                        kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
-                            make_float4(color.x, color.y, color.z, 1.0f);
-                    } else {
-                        float4 acc = kp.acc[slot_i];
-                        if (kp.accumulate) {  // AccumulationShader.shader:33, w = 1/FrameCount
-                            const float w = rcp_exact(float(smp.frame));
-                            const float k = 1.0f - w;
-                            acc = make_float4(acc.x * k + color.x * w, acc.y * k + color.y * w,
-                                              acc.z * k + color.z * w, acc.w * k + 1.0f * w);
-                        } else {
-                            acc = make_float4(color.x, color.y, color.z, 1.0f);
-                        }
-                        kp.acc[slot_i] = acc;
-                    }
-                    fs = (fs & 0xFFFF0000u) + 0x10000u;
-#if HG_STREAM_ITEMS
-                    const uint32_t k = items.take_here();
-                    if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
-                        uint32_t f;
-                        items.get(k, pix, f);
-                        next = true;
-                        sum = mk(0, 0, 0);
-                        fs = f << 16;
-                        smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u,
-                                      pcg_hash(items.tx0 + (pix & 7u) + (items.ty0 + (pix >> 3)) * kp.Wu), 0u};
-                        ms = MediumStack{0ull, 0};
-                    }
-#else
-                    if ((fs >> 16) < f_end) {  // next frame = next dispatch: statics reset
-                        next = true;
-                        sum = mk(0, 0, 0);
-                        smp.frame = kp.accumulate ? uint32_t(kp.first_frame) + (fs >> 16) : 1u;
-                        smp.offset = 0;
-                        ms = MediumStack{0ull, 0};
-                    }
+                    const size_t slot_i = kQueue ? size_t(slot) : size_t(uint32_t(local_tile)) * 64u + pix;
+                    // this frame's colour, blended later in frame order (hg_blend_frames)
+#if !HG_DIAG_NO_FC  // (analysis builds only: the write-traffic attribution of DESIGN.md §4.5)
+                    if (!fresh) kp.frame_color[fc_index(kp, fs >> 16, slot_i)] = make_float4(color.x, color.y, color.z, 1.0f);
 #endif
+                    fs = (fs & 0xFFFF0000u) + 0x10000u;
+                    if constexpr (kQueue) {
+                        uint32_t f = 0, hx = 0, hy = 0;
+                        if (queue_item(queue_take(), slot, f, hx, hy)) {  // the unit's next item: statics reset
+                            next = true;
+                            sum = mk(0, 0, 0);
+                            fs = f << 16;
+                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
+                                          0u};
+                            ms = MediumStack{0ull, 0};
+                        }
+                    } else {
+                        const uint32_t k = items.take_here();
+                        if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                            uint32_t f;
+                            items.get(k, pix, f);
+                            next = true;
+                            sum = mk(0, 0, 0);
+                            fs = f << 16;
+                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u,
+                                          pcg_hash(items.tx0 + (pix & 7u) + (items.ty0 + (pix >> 3)) * kp.Wu), 0u};
+                            ms = MediumStack{0ull, 0};
+                        }
+                    }
                 }
                 if (!one_sample) s_sum.set(sum);
                 if (next) {
                     {
-#if HG_STREAM_ITEMS
-                        const uint32_t qx = items.tx0 + (pix & 7u), qy = items.ty0 + (pix >> 3);
-#else
-                        const int gtile = kp.rank + local_tile * kp.n_ranks;
-                        const uint32_t qx = uint32_t(gtile % kp.tiles_x) * HG_TILE + (pix & 7u);
-                        const uint32_t qy = uint32_t(gtile / kp.tiles_x) * HG_TILE + (pix >> 3);
-#endif
+                        uint32_t qx, qy;
+                        if constexpr (kQueue) {
+                            slot_pixel(kp, slot, qx, qy);
+                        } else {
+                            qx = items.tx0 + (pix & 7u);
+                            qy = items.ty0 + (pix >> 3);
+                        }
                         ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     }
                     thr = mk(1, 1, 1);
@@ -853,7 +1054,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
-    const int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
+    int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
+    const bool queue = kp_in.queue != nullptr;  // the runtime passes a queue for launches of few frames
+    if (queue) grid = grid < int64_t(kp_in.resident_waves) ? grid : int64_t(kp_in.resident_waves);  // persistent waves
     if (grid == 0) return hipSuccess;
     const uint32_t lds_depth = kp_in.stack_depth < HG_STREAM_LDS_STACK ? kp_in.stack_depth : HG_STREAM_LDS_STACK;
     const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t) + HG_STREAM_LDS_PAD;
@@ -861,10 +1064,18 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     kp.mesh_lds_word = uint32_t(lds / 4u);
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
     const dim3 g{uint32_t(grid)}, b{64u};
-    if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true>), g, b, mesh_lds, stream, kp);
-    else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false>), g, b, lds, stream, kp);
-    else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true>), g, b, mesh_lds, stream, kp);
-    else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false>), g, b, lds, stream, kp);
+    const size_t sh = mesh_lds ? mesh_lds : lds;
+    if (queue) {
+        if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true, true>), g, b, sh, stream, kp);
+        else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false, true>), g, b, sh, stream, kp);
+        else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true, true>), g, b, sh, stream, kp);
+        else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false, true>), g, b, sh, stream, kp);
+    } else {
+        if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true, false>), g, b, sh, stream, kp);
+        else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false, false>), g, b, sh, stream, kp);
+        else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true, false>), g, b, sh, stream, kp);
+        else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false, false>), g, b, sh, stream, kp);
+    }
     return hipGetLastError();
 }
 

@@ -284,6 +284,7 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                                                                      ((bounce >> 16) & 0xFFu) > kp.max_trans);
                     }
                 } else {  // :941
+                    c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
                     col = col + sample_sky(kp, r.d, sky_level(kp, acc_rough)) * thr;
                 }
                 f3 sum = xyz(s4);
@@ -354,6 +355,8 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
             const uint32_t sv = wave_sum(v[k]);
             if (lane == 0 && sv) atomicAdd(kp.counters + k, (unsigned long long)sv);
         }
+        const uint32_t pm = wave_sum(c.primary_miss);
+        if (lane == 0 && pm) atomicAdd(kp.counters + 16, (unsigned long long)pm);
     }
 }
 

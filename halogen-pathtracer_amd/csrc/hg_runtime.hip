@@ -268,13 +268,33 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     return HG_OK;
 }
 
+// Wait for every stream of the context: the context stream and both trace streams (before device buffers that a
+// trace in flight may read are changed or freed)
+int quiesce(hg_ctx* c) {
+    HG_HIP(c, hipStreamSynchronize(c->stream));
+    for (hg_ctx::TraceLane& L : c->lanes)
+        if (L.stream) HG_HIP(c, hipStreamSynchronize(L.stream));
+    return HG_OK;
+}
+
+// Grow a trace stream's buffer; only when that buffer is not in use (quiesce first if it must move)
+int ensure_quiet(hg_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= std::max<size_t>(bytes, 16)) return HG_OK;
+    if (int rc = quiesce(c)) return rc;
+    return ensure(c, b, bytes);
+}
+
 int alloc_target(hg_ctx* c) {
+    if (int rc = quiesce(c)) return rc;
     c->tiles_x = (c->W + HG_TILE - 1) / HG_TILE;
     c->tiles_y = (c->H + HG_TILE - 1) / HG_TILE;
     const int64_t total = int64_t(c->tiles_x) * c->tiles_y;
     c->n_local_tiles = total > c->rank ? int32_t((total - c->rank + c->n_ranks - 1) / c->n_ranks) : 0;
-    c->tile_cost_valid = false;
-    c->tile_order_valid = false;
+    for (hg_ctx::TraceLane& L : c->lanes) {
+        L.tile_cost_valid = false;
+        L.tile_order_valid = false;
+        L.frames_since_order = 0;
+    }
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     const size_t slots = size_t(c->n_local_tiles) * 64;
 #if HG_WITH_VARIANTS  // wavefront pipeline path state (152 B per pixel slot)
@@ -405,23 +425,38 @@ int hg_create(int device, hg_ctx** out) {
     }
     c->n_cu = prop.multiProcessorCount;
     if (hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes) != hipSuccess) {
-        delete c;
+        hg_destroy(c);
         return HG_E_HIP;
     }
+    for (hg_ctx::TraceLane& L : c->lanes)
+        if (hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L.traced, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&L.blended, hipEventDisableTiming) != hipSuccess) {
+            hg_destroy(c);
+            return HG_E_HIP;
+        }
     *out = c;
     return HG_OK;
 }
 
 void hg_destroy(hg_ctx* c) {
     if (!c) return;
+    (void)hg_ctx_flush(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hg_ctx::TraceLane& L : c->lanes)
+        if (L.stream) (void)hipStreamSynchronize(L.stream);
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
                       &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->frame_color, &c->pool,
-                      &c->tile_cost, &c->tile_order})
+                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->pool})
         release(*b);
+    for (hg_ctx::TraceLane& L : c->lanes) {
+        for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.queue}) release(*b);
+        if (L.traced) (void)hipEventDestroy(L.traced);
+        if (L.blended) (void)hipEventDestroy(L.blended);
+        if (L.stream) (void)hipStreamDestroy(L.stream);
+    }
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
     for (auto& pr : c->pending_trace) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -437,6 +472,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
                     int32_t n_meshes, const PackedHalogenMaterial* materials, int32_t n_materials,
                     const HalogenTriangle* tris, int32_t n_tris, const BVHEntry* blas, int32_t n_nodes) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (n_spheres < 0 || n_meshes < 0 || n_materials < 0 || n_tris < 0 || n_nodes < 0)
         return fail(c, HG_E_INVALID, "negative count");
     if ((n_spheres && !spheres) || (n_meshes && !meshes) || (n_materials && !materials) || (n_tris && !tris) ||
@@ -449,6 +485,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if (n_materials > 255)
         return fail(c, HG_E_UNSUPPORTED, "at most 255 materials (medium stack packs material indices in bytes)");
     if (int rc = set_device(c)) return rc;
+    if (int rc = quiesce(c)) return rc;  // no trace in flight reads the buffers replaced below
     c->has_scene = false;
 
     // ---- spheres
@@ -620,6 +657,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
 
 int hg_upload_cubemap(hg_ctx* c, int32_t face_size, int32_t n_mips, const float* texels, size_t n_floats) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (face_size <= 0 || n_mips <= 0 || n_mips > HG_MAX_CUBE_MIPS || !texels)
         return fail(c, HG_E_INVALID, "bad cubemap shape");
     uint64_t need = 0;
@@ -631,6 +669,7 @@ int hg_upload_cubemap(hg_ctx* c, int32_t face_size, int32_t n_mips, const float*
     if (need != n_floats) return fail(c, HG_E_INVALID, "cubemap has %zu floats, expected %llu", n_floats,
                                       (unsigned long long)need);
     if (int rc = set_device(c)) return rc;
+    if (int rc = quiesce(c)) return rc;
     if (int rc = upload(c, c->cube, texels, n_floats * sizeof(float))) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     c->cube_size = face_size;
@@ -640,6 +679,7 @@ int hg_upload_cubemap(hg_ctx* c, int32_t face_size, int32_t n_mips, const float*
 
 int hg_set_params(hg_ctx* c, const hg_params* p) {
     if (!c || !p) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (p->samplesPerPixel < 1) return fail(c, HG_E_INVALID, "samplesPerPixel must be >= 1");
     if (!(p->screenParameters.x >= 1.0f) || !(p->screenParameters.y >= 1.0f))
         return fail(c, HG_E_INVALID, "screenParameters must be >= 1");
@@ -650,6 +690,7 @@ int hg_set_params(hg_ctx* c, const hg_params* p) {
 
 int hg_resize(hg_ctx* c, int32_t width, int32_t height) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (width <= 0 || height <= 0 || int64_t(width) * height > (int64_t(1) << 31))
         return fail(c, HG_E_INVALID, "bad target size %dx%d", width, height);
     if (int rc = set_device(c)) return rc;
@@ -660,6 +701,7 @@ int hg_resize(hg_ctx* c, int32_t width, int32_t height) {
 
 int hg_set_tiling(hg_ctx* c, int32_t rank, int32_t n_ranks) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(c, HG_E_INVALID, "bad tiling %d/%d", rank, n_ranks);
     if (int rc = set_device(c)) return rc;
     c->rank = rank;
@@ -669,13 +711,34 @@ int hg_set_tiling(hg_ctx* c, int32_t rank, int32_t n_ranks) {
 
 int hg_clear_accumulation(hg_ctx* c) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
     if (c->acc.p) HG_HIP(c, hipMemsetAsync(c->acc.p, 0, c->acc.bytes, c->stream));
     return HG_OK;
 }
 
-int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
-    if (!c) return HG_E_INVALID;
+}  // extern "C"
+
+namespace {
+
+// Validation of an hg_render call against the context's state (at the call, so that errors come from the call itself)
+int render_check(hg_ctx* c, int32_t n_frames) {
+    if (!c->has_scene) return fail(c, HG_E_NOSCENE, "hg_upload_scene not called");
+    if (!c->has_params) return fail(c, HG_E_INVALID, "hg_set_params not called");
+    if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
+    if (n_frames < 0) return fail(c, HG_E_INVALID, "n_frames < 0");
+    const hg_params& p = c->params;
+    if (int32_t(p.screenParameters.x) != c->W || int32_t(p.screenParameters.y) != c->H)
+        return fail(c, HG_E_INVALID, "screenParameters (%g,%g) != target %dx%d", p.screenParameters.x,
+                    p.screenParameters.y, c->W, c->H);
+    const int32_t ns = int32_t(p.bufferCounts.x), nm = int32_t(p.bufferCounts.y);
+    if (ns < 0 || ns > c->n_spheres || nm < 0 || nm > c->n_meshes)
+        return fail(c, HG_E_INVALID, "bufferCounts (%d,%d) exceed uploaded (%d,%d)", ns, nm, c->n_spheres, c->n_meshes);
+    return HG_OK;
+}
+
+// One launch of n_frames frames from FrameCount = params.frameCount (which it advances when accumulating)
+int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (!c->has_scene) return fail(c, HG_E_NOSCENE, "hg_upload_scene not called");
     if (!c->has_params) return fail(c, HG_E_INVALID, "hg_set_params not called");
     if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
@@ -818,18 +881,14 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         }
         if (units > 0) split = int(std::min<int64_t>(split, kMaxWaves / units));
         int chunk_max = HG_REGEN_MAX_CHUNK;
-        // frame colours, blended after the launch (frame split, or item scheduling of a multi-frame launch; a 1-frame
-        // launch blends each pixel's one item straight into the accumulator)
-        const bool items_k = regen && !pool_k && (stream_k ? HG_STREAM_ITEMS : HG_REGEN_ITEMS);
-        const bool colours = split > 1 || (items_k && n_frames > 1);
-        if (colours) {
-            const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
+        // The streaming kernel (always) and the regenerating kernel (item scheduling or a frame split) store every
+        // frame's colour and blend them into the accumulator in frame order afterwards (hg_blend_frames): such a launch
+        // is traced on a trace stream and blended on the context stream (the trace pipeline, hg_ctx.h).
+        const bool items_k = regen && !pool_k && (stream_k || HG_REGEN_ITEMS);
+        const bool pipelined = regen && !pool_k && (items_k || split > 1);
+        const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
+        if (pipelined)
             chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
-            if (int rc = ensure(c, c->frame_color, per_frame * size_t(std::min(n_frames, chunk_max)))) {
-                c->free_events.push_back(ev);
-                return rc;
-            }
-        }
         const int mgrid = int((units * split + mblock / 64 - 1) / (mblock / 64));
         if (pool_k) {
             if (int rc = ensure(c, c->pool, size_t(mgrid) * hg_pool_slots() * 8 * sizeof(float4))) {
@@ -841,8 +900,10 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
         // stack entries beyond the LDS part: one column per thread (the streaming kernel's LDS part may be shorter)
         const uint32_t lds_part = std::min<uint32_t>(HG_MEGA_LDS_STACK, HG_STREAM_LDS_STACK);
-        if (kp.stack_depth > lds_part) {
-            if (int rc = ensure(c, c->wf_spill, size_t(kp.spill_stride) * (kp.stack_depth - lds_part) * 4)) {
+        const size_t spill_bytes =
+            kp.stack_depth > lds_part ? size_t(kp.spill_stride) * (kp.stack_depth - lds_part) * 4 : 0;
+        if (spill_bytes && !pipelined) {
+            if (int rc = ensure_quiet(c, c->wf_spill, spill_bytes)) {
                 c->free_events.push_back(ev);
                 return rc;
             }
@@ -851,55 +912,89 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
 
         c->counters.last_kernel = uint64_t(regen ? kern : HG_KERNEL_MEGA);
         hipError_t e = hipSuccess;
-        if (regen) {  // frames are independent dispatches: chunking at frame boundaries changes nothing
-            HgKernelParams kc = kp;
-            kc.frame_color = static_cast<float4*>(c->frame_color.p);
-            // cost-ordered dispatch: the previous launch's per-tile wave times order this launch's tiles, most
-            // expensive first, so the launch's drain tail holds the cheap tiles (any order gives the same image)
-            kc.tile_cost = nullptr;
-            kc.tile_order = nullptr;
-            if (c->tile_order_on && tiles > 0 && !pool_k) {
-                const size_t tb = size_t(tiles) * sizeof(uint32_t);
-                if (int rc = ensure(c, c->tile_cost, 2 * tb)) {
+        const bool ordered = pipelined && c->tile_order_on && tiles > 0;
+        const size_t tb = size_t(tiles) * sizeof(uint32_t);
+        if (pipelined) {
+            // both trace streams' buffers, grown only while idle
+            for (hg_ctx::TraceLane& L : c->lanes) {
+                int rc = ensure_quiet(c, L.frame_color, per_frame * size_t(std::min(n_frames, chunk_max)));
+                if (!rc && spill_bytes) rc = ensure_quiet(c, L.spill, spill_bytes);
+                if (!rc && ordered) rc = ensure_quiet(c, L.tile_cost, 2 * tb);
+                if (!rc && ordered) rc = ensure_quiet(c, L.tile_order, tb);
+                if (!rc && stream_k) rc = ensure_quiet(c, L.queue, 8 * 128);
+                if (rc) {
                     c->free_events.push_back(ev);
                     return rc;
                 }
-                if (int rc = ensure(c, c->tile_order, tb)) {
-                    c->free_events.push_back(ev);
-                    return rc;
-                }
-                kc.tile_cost = static_cast<unsigned long long*>(c->tile_cost.p);
             }
+            HgKernelParams kc = kp;
+            kc.resident_waves = uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES;
+            for (int done = 0; done < n_frames && e == hipSuccess;) {  // chunks at frame boundaries change nothing
+                hg_ctx::TraceLane& L = c->lanes[c->next_lane];
+                c->next_lane = (c->next_lane + 1) % HG_TRACE_LANES;
+                kc.n_frames = std::min(n_frames - done, chunk_max);
+                kc.first_frame = accumulate ? kp.first_frame + done : 1;
+                kc.frame_split = std::min(split, kc.n_frames);
+                kc.frame_color = static_cast<float4*>(L.frame_color.p);
+                kc.spill = spill_bytes ? static_cast<uint32_t*>(L.spill.p) : nullptr;
+                // the persistent work-queue form for launches of few frames (the reference's one dispatch per frame)
+                kc.queue = stream_k && kc.n_frames <= HG_QUEUE_MAX_FRAMES ? static_cast<uint32_t*>(L.queue.p) : nullptr;
+                kc.tile_order = nullptr;
+                kc.tile_cost = ordered ? static_cast<unsigned long long*>(L.tile_cost.p) : nullptr;
+                // this stream's buffers are free once the blend of its previous chunk has read them
+                if (L.blend_pending) e = hipStreamWaitEvent(L.stream, L.blended, 0);
+                if (e == hipSuccess && done == 0) e = hipEventRecord(ev.first, L.stream);  // the launch starts here
+                if (e == hipSuccess && ordered) {
+                    // Cost order, per trace stream: the stream sorts its own costs into its own order buffer (the
+                    // traces adding those costs and reading that order run on the same stream, so none is in flight
+                    // during the sort), once HG_ORDER_MIN_FRAMES frames were traced on it since its last sort:
+                    // 64-frame launches every time, the reference's 1-frame launches every 16th frame per stream.
+                    if (L.tile_cost_valid &&
+                        (!L.tile_order_valid || L.frames_since_order >= int64_t(HG_ORDER_MIN_FRAMES))) {
+                        e = hg_launch_order_tiles(kc.tile_cost, static_cast<uint32_t*>(L.tile_order.p), uint32_t(tiles),
+                                                  L.stream);
+                        L.tile_order_valid = e == hipSuccess;
+                        L.frames_since_order = 0;
+                    } else if (!L.tile_cost_valid) {
+                        e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(unsigned long long), L.stream);
+                        L.tile_order_valid = false;
+                        L.frames_since_order = 0;
+                    }
+                    if (L.tile_order_valid) kc.tile_order = static_cast<const uint32_t*>(L.tile_order.p);
+                    L.tile_cost_valid = e == hipSuccess;
+                    L.frames_since_order += kc.n_frames;
+                }
+                if (e == hipSuccess && kc.queue) e = hipMemsetAsync(kc.queue, 0, 8 * 128, L.stream);
+                std::pair<hipEvent_t, hipEvent_t> tev{};
+                if (e == hipSuccess && c->timing) {
+                    if (int rc = event_pair(c, tev)) {
+                        c->free_events.push_back(ev);
+                        return rc;
+                    }
+                    e = hipEventRecord(tev.first, L.stream);
+                }
+                if (e == hipSuccess)
+                    e = stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, L.stream)
+                                 : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, L.stream);
+                if (e == hipSuccess && c->timing) {
+                    e = hipEventRecord(tev.second, L.stream);
+                    c->pending_trace.push_back(tev);
+                }
+                if (e == hipSuccess) e = hipEventRecord(L.traced, L.stream);
+                if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, L.traced, 0);
+                if (e == hipSuccess) e = hg_launch_blend_frames(kc, c->stream);  // in frame order, on the context stream
+                if (e == hipSuccess) e = hipEventRecord(L.blended, c->stream);
+                L.blend_pending = e == hipSuccess;
+                done += kc.n_frames;
+            }
+        } else if (regen) {  // the path pool, or a regenerating launch that blends in the kernel: on the context stream
+            HgKernelParams kc = kp;
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
-                if (kc.tile_cost) {
-                    // Sort from the recorded costs (which the sort clears) once HG_ORDER_MIN_FRAMES frames' worth have
-                    // accumulated, or when no order exists yet; in between, launches keep the last order and add to
-                    // the costs.  A 64-frame launch sorts every time; the drop-in's 1-frame launches (RP:327) pay the
-                    // 0.1-ms sort once per 16 frames instead of once per frame.
-                    if (c->tile_cost_valid &&
-                        (!c->tile_order_valid || c->frames_since_order >= int64_t(HG_ORDER_MIN_FRAMES))) {
-                        e = hg_launch_order_tiles(kc.tile_cost, static_cast<uint32_t*>(c->tile_order.p),
-                                                  uint32_t(tiles), c->stream);
-                        c->tile_order_valid = e == hipSuccess;
-                        c->frames_since_order = 0;
-                    } else if (!c->tile_cost_valid) {
-                        e = hipMemsetAsync(kc.tile_cost, 0, size_t(tiles) * sizeof(unsigned long long), c->stream);
-                        c->tile_order_valid = false;
-                        c->frames_since_order = 0;
-                    }
-                    if (c->tile_order_valid) kc.tile_order = static_cast<const uint32_t*>(c->tile_order.p);
-                    c->tile_cost_valid = e == hipSuccess;
-                    c->frames_since_order += kc.n_frames;
-                }
-                if (e == hipSuccess)
-                    e = pool_k     ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
-                    : stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, c->stream)
-                               : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
-                if (e == hipSuccess && (kc.frame_split > 1 || (items_k && kc.n_frames > 1)))
-                    e = hg_launch_blend_frames(kc, c->stream);
+                e = pool_k ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
+                           : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
                 done += kc.n_frames;
             }
         } else {
@@ -926,10 +1021,37 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     return HG_OK;
 }
 
+}  // namespace
+
+int hg_ctx_flush(hg_ctx* c) {
+    if (!c || c->pending_frames == 0) return HG_OK;
+    const int32_t n = c->pending_frames, acc = c->pending_acc;
+    c->pending_frames = 0;
+    return render_now(c, n, acc);
+}
+
+extern "C" {
+
+int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = render_check(c, n_frames)) return rc;
+    if (n_frames == 0) return HG_OK;
+    accumulate = accumulate ? 1 : 0;
+    if (c->pending_frames > 0 && (accumulate != c->pending_acc || int64_t(c->pending_frames) + n_frames > INT32_MAX))
+        if (int rc = hg_ctx_flush(c)) return rc;
+    if (c->coalesce <= 1 && c->pending_frames == 0) return render_now(c, n_frames, accumulate);
+    // held: the frames follow the held ones (FrameCount advances at the launch; nothing reads it before, every other
+    // entry point flushes first)
+    c->pending_acc = accumulate;
+    c->pending_frames += n_frames;
+    return c->pending_frames >= c->coalesce ? hg_ctx_flush(c) : HG_OK;
+}
+
 int hg_synchronize(hg_ctx* c) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
-    HG_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc = quiesce(c)) return rc;
     return drain_events(c);
 }
 
@@ -937,6 +1059,7 @@ int32_t hg_local_tile_count(const hg_ctx* c) { return c ? c->n_local_tiles : 0; 
 
 int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
     if (!c || !rgba) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
     if (n_floats < size_t(c->W) * size_t(c->H) * 4) return fail(c, HG_E_INVALID, "readback buffer too small");
     if (int rc = set_device(c)) return rc;
@@ -964,6 +1087,7 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
 
 int hg_set_accumulation(hg_ctx* c, const float* rgba, size_t n_floats, int32_t frame_count) {
     if (!c || !rgba) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
     if (n_floats < size_t(c->W) * size_t(c->H) * 4) return fail(c, HG_E_INVALID, "accumulation image too small");
     if (frame_count < 1) return fail(c, HG_E_INVALID, "frame_count must be >= 1 (FrameCount starts at 1, RP:152)");
@@ -989,6 +1113,7 @@ int hg_set_accumulation(hg_ctx* c, const float* rgba, size_t n_floats, int32_t f
 
 int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
     if (!c || !dst) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     const size_t need = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     if (n_bytes < need) return fail(c, HG_E_INVALID, "destination too small (%zu < %zu)", n_bytes, need);
     if (int rc = set_device(c)) return rc;
@@ -1001,6 +1126,7 @@ int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
 int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     hg_ctx* c = const_cast<hg_ctx*>(cc);
     if (!c || !out) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (int rc = drain_events(c)) return rc;
@@ -1027,6 +1153,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
 
 int hg_reset_counters(hg_ctx* c) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (int rc = drain_events(c)) return rc;
@@ -1050,6 +1177,7 @@ int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
 
 int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
     switch (option) {
         case HG_OPT_KERNEL:
             if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
@@ -1079,8 +1207,11 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             return HG_OK;
         case HG_OPT_TILE_ORDER:
             c->tile_order_on = value ? 1 : 0;
-            c->tile_cost_valid = false;
-            c->tile_order_valid = false;
+            for (hg_ctx::TraceLane& L : c->lanes) L.tile_cost_valid = L.tile_order_valid = false;
+            return HG_OK;
+        case HG_OPT_COALESCE:
+            if (value < 1 || value > 65535) return fail(c, HG_E_INVALID, "coalesce window must be 1..65535 frames");
+            c->coalesce = value;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void hg_wf_shade(const HgKernelParams kp, cons
                                                    const uint32_t* __restrict__ n_in, uint32_t* __restrict__ q_out,
                                                    uint32_t* __restrict__ n_out) {
     const uint32_t n = *n_in;
-    uint32_t c_hits = 0, c_paths = 0;
+    uint32_t c_hits = 0, c_paths = 0, c_pmiss = 0;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
         const uint32_t qi = base + threadIdx.x;
@@ -406,6 +406,8 @@ __global__ __launch_bounds__(256) void hg_wf_shade(const HgKernelParams kp, cons
                                                             bounce.transmission > kp.max_trans);
                 }
             } else {
+                // the path's camera ray: no bounce accepted yet (iter counts the rays after the first)
+                c_pmiss += iter == 0u && bounce.diffuse == 0u && bounce.glossy == 0u && bounce.transmission == 0u;
                 col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;  // :941
             }
 
@@ -471,6 +473,8 @@ __global__ __launch_bounds__(256) void hg_wf_shade(const HgKernelParams kp, cons
     if (kp.counters) {
         const uint32_t v[7] = {c_paths, 0, 0, 0, 0, 0, c_hits};
         wave_add_counters(kp, v);
+        const uint32_t pm = wave_sum(c_pmiss);
+        if (lane_id() == 0 && pm) atomicAdd(kp.counters + 16, (unsigned long long)pm);
     }
 }
 

@@ -95,6 +95,7 @@ HG_KERNEL_AUTO = 5
 HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING, HG_OPT_REFILL, HG_OPT_FRAME_SPLIT = 1, 2, 3, 4, 5, 6
 HG_OPT_DESCENT_T = 7
 HG_OPT_TILE_ORDER = 8
+HG_OPT_COALESCE = 9
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [
@@ -163,6 +164,12 @@ def lib() -> C.CDLL:
         "hg_comm_destroy": (None, [P]),
     }
     for name, (res, args) in sig.items():
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if not os.environ.get("HALOGEN_LIB"):
+                raise
+            continue  # an older A/B build (tools/sweeps) without this entry point
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

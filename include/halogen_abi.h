@@ -189,7 +189,9 @@ enum {
 /* AUTO (default): MEGA_STREAM when the scene has a BLAS deeper than 16 levels, else MEGA_REGEN. */
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
        HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5 };
-/* HG_OPT_BLOCK: workgroup size of the traversal kernel (64/128/256).  HG_OPT_COUNTERS: work counters on/off.
+/* HG_OPT_BLOCK: workgroup size of the lockstep kernel HG_KERNEL_MEGA (64/128/256; the debug views, large-maxBounces
+ *   fallback) and of the wavefront trace kernel; the regenerating / streaming / pool kernels always run one-wave
+ *   workgroups (their per-lane LDS rows assume it) and ignore it.  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).
  * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then
@@ -199,9 +201,14 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   test their leaves meanwhile; each lane's own step order is unchanged): -1 = automatic (for BLAS deeper than 16
  *   levels 3, or 8 with the streaming kernel; else 0 = classic while-while), 0..64 = fixed.
  * HG_OPT_TILE_ORDER: regenerating / streaming kernels, 1 (default) = each launch dispatches its tiles by descending
- *   wave time in the previous launch (shorter drain tail; same image), 0 = tile-index order. */
+ *   wave time in the previous launches (shorter drain tail; same image), 0 = tile-index order.
+ * HG_OPT_COALESCE: hg_render is asynchronous, so consecutive calls (same parameters, same accumulate flag) are held and
+ *   launched together once this many frames are pending (default 32), or as soon as any other entry point is called
+ *   (each launches the held frames first).  The frames, their order and the image are those of separate launches; a
+ *   launch has a fixed cost (its drain tail: ~0.35 ms on C3), so the reference's one call per frame (RP:327) runs at
+ *   the multi-frame rate.  1 = every call launches at once. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8 };
+       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9 };
 
 int hg_abi_version(void);
 
@@ -237,7 +244,7 @@ int hg_clear_accumulation(hg_ctx* ctx);
 /* Trace n_frames consecutive frames, FrameCount = params.frameCount + k, each followed by the
  * progressive blend acc = acc*(1-w) + new*w with w = 1.0f/FrameCount (AccumulationShader.shader:33).
  * accumulate == 0 reproduces Accumulate=false: FrameCount forced to 1 and acc = new each frame.
- * Asynchronous on the context stream. */
+ * Asynchronous on the context stream (the frames may be held for one launch with later calls: HG_OPT_COALESCE). */
 int hg_render(hg_ctx* ctx, int32_t n_frames, int32_t accumulate);
 
 int hg_synchronize(hg_ctx* ctx);
@@ -263,7 +270,7 @@ int32_t hg_local_tile_count(const hg_ctx* ctx);
 int hg_get_counters(const hg_ctx* ctx, hg_counters* out);
 int hg_reset_counters(hg_ctx* ctx);
 
-/* Tuning knobs (kernel variant, block size, counters on/off). */
+/* Tuning knobs (kernel variant, lockstep block size, counters on/off, ...: the HG_OPT_* above). */
 int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
 
 /* Device self-tests of arithmetic shortcuts the kernels rely on (and the build's compiled-in checks).  HG_SELFTEST_RCP: the fast correctly-rounded

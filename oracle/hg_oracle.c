@@ -441,11 +441,23 @@ void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t 
         g_stack_max = 0;
     }
 }
+/* the popped node was the mesh's root: the stack was empty after its pop and nothing had been pushed before */
+static int stack_is_root(int sp, int high) { return sp == 0 && high == 1; }
 static void note_stack(int high) {
     if (high > REF_NODE_STACK) g_stack_overflow_traversals++;
     int32_t cur = g_stack_max;
     while (high > cur && !__atomic_compare_exchange_n((int32_t*)&g_stack_max, &cur, high, 0, __ATOMIC_RELAXED,
                                                        __ATOMIC_RELAXED)) {
+    }
+}
+
+/* Diagnostics (test infra, tools/visit_stats.py): inner-node visits by how many of the two children the exact test
+ * keeps (t < closest), for mesh roots and for deeper nodes: [root 0/1/2, inner 0/1/2]. */
+static _Atomic uint64_t g_visit_ok[6];
+void hgo_visit_stats(uint64_t out[6], int32_t reset) {
+    for (int k = 0; k < 6; ++k) {
+        if (out) out[k] = g_visit_ok[k];
+        if (reset) g_visit_ok[k] = 0;
     }
 }
 
@@ -490,6 +502,7 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
                 float dB = ray_aabb(fromv(B->boundingCornerA), fromv(B->boundingCornerB), &pre);
                 t->aabb_tests += 2;
                 t->cnt.aabb_tests += 2;
+                g_visit_ok[(stack_is_root(sp, high) ? 0 : 3) + (dA < closest.rayT) + (dB < closest.rayT)]++;
                 /* pushes beyond NODE_STACK are dropped; hg_upload_scene rejects trees deep enough to
                  * reach that, so this is a guard, not behaviour */
                 if (dB < dA) {

@@ -65,6 +65,8 @@ void hgo_trace_pixel(const hgo_scene* scene, const hg_params* params, uint32_t x
 /* Diagnostics: mesh traversals (since the last reset) whose node stack would hold more than the reference's
  * NodeStack[32] entries (HC:397), and the deepest stack seen. */
 void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t reset);
+/* Diagnostics: inner-node visits by the number of children the exact test keeps: [root 0/1/2, inner 0/1/2]. */
+void hgo_visit_stats(uint64_t out[6], int32_t reset);
 
 /* Per-stage KAT entry points */
 float hgo_sphere_t(const float o[3], const float d[3], const float c[3], float r);

@@ -73,6 +73,8 @@ def lib():
         L.hgo_aabb_t.argtypes = [fp, fp, fp, fp]
         L.hgo_stack_stats.restype = None
         L.hgo_stack_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_int32), C.c_int32]
+        L.hgo_visit_stats.restype = None
+        L.hgo_visit_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int32]
         L.hgo_cube_sample.restype = None
         L.hgo_cube_sample.argtypes = [C.POINTER(HgoScene), fp, C.c_int32, fp]
         L.hgo_cube_adjacent.restype = None
@@ -135,6 +137,13 @@ def stack_stats(reset: bool = False) -> tuple[int, int]:
     n, d = C.c_uint64(0), C.c_int32(0)
     lib().hgo_stack_stats(C.byref(n), C.byref(d), 1 if reset else 0)
     return int(n.value), int(d.value)
+
+
+def visit_stats(reset: bool = False) -> dict:
+    """Inner-node visits by the number of children the exact test keeps (0/1/2), for mesh roots and deeper nodes."""
+    out = (C.c_uint64 * 6)()
+    lib().hgo_visit_stats(out, 1 if reset else 0)
+    return {"root": [int(x) for x in out[:3]], "inner": [int(x) for x in out[3:]]}
 
 
 def cube_adjacent(face: int, i: int, j: int, size: int) -> tuple[int, int, int]:

@@ -100,17 +100,19 @@ try:
     abi.Comm.rank(ctx, 2, abi.comm_unique_id(), 0)  # rank 1 never joins
     print("JOINED")
 except abi.HalogenError as e:
-    print("FAILED-LOUDLY %.1f %s" % (time.time() - t0, e))
+    print("FAILED-LOUDLY %.1f %s" % (time.time() - t0, e), flush=True)
 ctx.close()
+import os
+os._exit(0)  # the abandoned init's helper thread may still be blocked in RCCL: do not wait for it at exit
 """
 
 
 @pytest.mark.gpu
 def test_gpu_comm_dead_peer_fails_within_deadline(gpu, tmp_path):
-    """A 2-rank communicator whose second rank never joins: hg_comm_init_rank (non-blocking RCCL init polled with
-    ncclCommGetAsyncError) gives up at the deadline (HALOGEN_COMM_TIMEOUT_MS), aborts the communicator and returns
-    HG_E_COMM with text, instead of blocking forever.  Run in a child process so that a hang could not take the test
-    session with it."""
+    """A 2-rank communicator whose second rank never joins: hg_comm_init_rank (ncclCommInitRank on a helper thread,
+    waited for with the deadline HALOGEN_COMM_TIMEOUT_MS) gives up at the deadline and returns HG_E_COMM with text,
+    instead of blocking forever (RCCL's own non-blocking init was measured to block in the caller while a peer is
+    missing).  Run in a child process so that a hang could not take the test session with it."""
     import os
     import subprocess
     import sys
@@ -123,7 +125,7 @@ def test_gpu_comm_dead_peer_fails_within_deadline(gpu, tmp_path):
     assert "FAILED-LOUDLY" in r.stdout, out[-2000:]
     secs = float(r.stdout.split("FAILED-LOUDLY")[1].split()[0])
     assert 2.5 <= secs < 60, out[-2000:]
-    assert "communicator aborted" in r.stdout and "3000 ms" in r.stdout, out[-2000:]
+    assert "did not all join within 3000 ms" in r.stdout, out[-2000:]
 
 
 @pytest.mark.gpu

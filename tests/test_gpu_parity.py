@@ -23,10 +23,12 @@ if os.environ.get("HG_TEST_VARIANTS") == "1":  # library built with make VARIANT
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="auto",
-               block=None):
+               block=None, coalesce=None):
     own = ctx is None
     ctx = ctx or abi.Context(0)
     ctx.set_option(abi.HG_OPT_KERNEL, KERNELS[kernel])
+    if coalesce:
+        ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
     if block:
         ctx.set_option(abi.HG_OPT_BLOCK, block)
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)

@@ -1,9 +1,11 @@
 """The drop-in's operating point and its checkpoint state, through the C-ABI.
 
 The reference dispatches HalogenCompute once per frame (RP:327, dispatch RP:406) and blends it into the accumulation
-target (RP:343-347); hg_render(n) runs n such frames in one launch.  A 1-frame launch takes its own path through the
-kernels (each pixel's one item blends straight into the accumulator, no frame-colour buffer, no blend pass; the tile
-order is re-sorted only every HG_ORDER_MIN_FRAMES frames), so it is checked bit for bit against the batched launch.
+target (RP:343-347); hg_render(n) runs n such frames in one launch.  Launches of few frames take their own path through
+the kernels (the streaming kernel's persistent work-queue form, the lean blend, the tile order re-sorted every
+HG_ORDER_MIN_FRAMES frames per trace stream, traces of consecutive launches overlapping on two streams), and
+consecutive hg_render calls are held and launched together (HG_OPT_COALESCE) until something observes the state; both
+are checked bit for bit against the batched launch: strict (coalesce 1: every call its own launch) and coalesced.
 
 Checkpoint/resume: the reference's resumable state is the accumulation target plus FrameCount (RP:152, 185, 347);
 hg_readback exports it and hg_set_accumulation restores it into a fresh context."""
@@ -32,18 +34,53 @@ def _full(cfg_name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("coalesce", [1, 3, 16])
 @pytest.mark.parametrize("name", ["dragon10_64x36", "glass_64x36", "c1_64", "c1_48_noacc", "c1_64_spp3"])
-def test_gpu_one_frame_launches_match_golden(gpu, name):
+def test_gpu_one_frame_launches_match_golden(gpu, name, coalesce):
     """frames x hg_render(1) (the reference's per-frame dispatches) equals the golden image and counters, and the
     batched hg_render(frames), for the streaming (dragon, Cornell) and regenerating (glass) kernels, without
-    accumulation and with spp 3."""
+    accumulation and with spp 3; every call its own launch (coalesce 1) or held 3 / 16 frames at a time."""
     meta = json.loads((GOLD / f"{name}.json").read_text())
     packed, params, cube, frames, acc = cases.setup(name)
-    img, cnt = gpu_render(packed, params, frames, acc, cube, splits=[1] * frames)
-    assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name} as {frames} x render(1)")
+    img, cnt = gpu_render(packed, params, frames, acc, cube, splits=[1] * frames, coalesce=coalesce)
+    assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name} as {frames} x render(1), coalesce {coalesce}")
     for k, v in meta["counters"].items():
         assert cnt[k] == v, (k, cnt[k], v)
-    assert cnt["launches"] == frames
+    assert cnt["launches"] == -(-frames // coalesce)
+
+
+@pytest.mark.gpu
+def test_gpu_coalesced_frames_flush_at_every_observation(gpu):
+    """Held frames are launched before anything reads or changes the context: a readback after 3 held calls is the
+    3-frame image; a counters read, set_params with a new camera, clear_accumulation and set_accumulation all see the
+    held frames first."""
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    three, c3 = gpu_render(packed, params, 3, True, cube)
+    five, _ = gpu_render(packed, params, 5, True, cube)
+    with abi.Context(0) as ctx:
+        ctx.set_option(abi.HG_OPT_COALESCE, 64)
+        ctx.upload_scene(packed)
+        ctx.resize(W, H)
+        ctx.set_params(params)
+        for _ in range(3):
+            ctx.render(1, True)
+        assert_bitwise(ctx.readback(W, H), three, "readback after 3 held frames")
+        for _ in range(2):
+            ctx.render(1, True)
+        assert ctx.counters()["paths"] == c3["paths"] // 3 * 5  # the held frames ran before the read
+        assert_bitwise(ctx.readback(W, H), five, "5 frames")
+        ctx.render(1, True)
+        ctx.clear_accumulation()  # launches the held frame first, then clears
+        ctx.set_params(params)
+        for _ in range(3):
+            ctx.render(1, True)
+        ctx.set_params(params)  # launches the 3 held frames (FrameCount 1..3), then resets FrameCount to 1
+        assert_bitwise(ctx.readback(W, H), three, "held frames launched by set_params")
+        ctx.render(2, True)
+        ctx.set_accumulation(three, 4)  # the 2 held frames land first, then the checkpoint overwrites them
+        ctx.render(2, True)
+        assert_bitwise(ctx.readback(W, H), five, "checkpoint after held frames")
 
 
 @pytest.mark.gpu
@@ -55,14 +92,15 @@ def test_gpu_one_frame_launches_match_batched_full_size(gpu, cfg_name):
     packed, params, cube = _full(cfg_name)
     frames = 64
     batched, bc = gpu_render(packed, params, frames, True, cube)
-    single, sc = gpu_render(packed, params, frames, True, cube, splits=[1] * frames)
-    assert_bitwise(single, batched, f"{cfg_name}: 64 x render(1) vs render(64)")
-    for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
-        assert sc[k] == bc[k], (k, sc[k], bc[k])
+    for coalesce in (1, 16):
+        single, sc = gpu_render(packed, params, frames, True, cube, splits=[1] * frames, coalesce=coalesce)
+        assert_bitwise(single, batched, f"{cfg_name}: 64 x render(1) vs render(64), coalesce {coalesce}")
+        for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+            assert sc[k] == bc[k], (k, sc[k], bc[k])
     W = int(params.screenParameters.x)
     y0, y1 = 538, 540
     ref, _ = hg_oracle.render(packed, params, 2, True, cubemap=cube, pix_range=(y0 * W, y1 * W))
-    two, _ = gpu_render(packed, params, 2, True, cube, splits=[1, 1])
+    two, _ = gpu_render(packed, params, 2, True, cube, splits=[1, 1], coalesce=1)
     assert_bitwise(two[y0:y1], ref[y0:y1], f"{cfg_name} rows {y0}-{y1}, 2 x render(1) vs oracle")
 
 
@@ -73,8 +111,10 @@ def test_gpu_mixed_launch_sizes_with_tile_order(gpu):
     packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
     for tiling in (None, (1, 3)):
         ref, _ = gpu_render(packed, params, 40, True, cube, tiling=tiling)
-        img, _ = gpu_render(packed, params, 40, True, cube, tiling=tiling, splits=[1] * 17 + [5] + [1] * 18)
-        assert_bitwise(img, ref, f"mixed launches, tiling {tiling}")
+        for coalesce in (1, 4):
+            img, _ = gpu_render(packed, params, 40, True, cube, tiling=tiling, splits=[1] * 17 + [5] + [1] * 18,
+                                coalesce=coalesce)
+            assert_bitwise(img, ref, f"mixed launches, tiling {tiling}, coalesce {coalesce}")
 
 
 @pytest.mark.gpu
