@@ -71,22 +71,31 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
     ctx.clear_accumulation()
     ctx.set_params(params)
     ctx.synchronize()
+    ctx.reset_counters()
     t0 = time.perf_counter()
     for _ in range(steps):
         ctx.render(frames_per_step, True)
     ctx.synchronize()
     dt = time.perf_counter() - t0
+    timing = ctx.counters()  # trace-kernel launch durations (HIP events on the trace streams)
     ctx.clear_accumulation()
     ctx.set_params(params)
     ctx.reset_counters()
     ctx.set_option(abi.HG_OPT_COUNTERS, 1)
     ctx.render(frames_per_step, True)
     c = ctx.counters()
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
     paths = W * H * frames_per_step * steps
+    kernel_symbol = KERNEL_SYMBOL.get(int(c["last_kernel"]), "?")
+    mean_launch_s = timing["trace_ms"] / max(timing["trace_launches"], 1) / 1e3
+    # its own roofline, from the committed C3F PMC pass (profiles/pmc_traffic_C3F.json)
+    roofline = roofline_of(committed_counters("C3F", W, H, frames_per_step, kernel_symbol), mean_launch_s,
+                           algorithmic_bytes(c), kernel_symbol, dt / steps)
     return {"workload": cfg.name, "value": paths / dt / 1e6, "unit": "Mpaths/s", "steps": steps,
             "ms_per_step": dt * 1e3 / steps, "mrays_per_s": c["rays"] / c["paths"] * paths / dt / 1e6,
             "primary_miss_frac": c["primary_misses"] / c["paths"], "rays_per_path": c["rays"] / c["paths"],
-            "tri_tests_per_path": c["tri_tests"] / c["paths"], "camera_position": list(scenes.CORNELL_FRAMED_CAMERA_POS)}
+            "tri_tests_per_path": c["tri_tests"] / c["paths"], "camera_position": list(scenes.CORNELL_FRAMED_CAMERA_POS),
+            "roofline": roofline}
 
 
 def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_value: float) -> dict:
@@ -148,6 +157,25 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
             "with_readback": {"value": paths / dt_rb / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_rb * 1e3 / frames,
                               "readback_bytes_per_frame": W * H * 16},
             "bit_identical_to_batched": identical}
+
+
+def committed_counters(config: str, W: int, H: int, frames_per_launch: int, kernel_symbol: str) -> dict:
+    """The committed PMC figures of this workload's production kernel (tools/summarize_profile.py):
+    profiles/pmc_traffic_<config>.json, or profiles/pmc_traffic.json (the headline config's), when they match the
+    config, image size, frames per launch and the counter-free instantiation of the kernel that ran."""
+    for name in (f"pmc_traffic_{config}.json", "pmc_traffic.json"):
+        f = ROOT / "profiles" / name
+        if not f.exists():
+            continue
+        try:
+            t = json.loads(f.read_text())
+        except Exception:
+            continue
+        if (t.get("config") == config and t.get("width") == W and t.get("height") == H
+                and t.get("frames_per_launch") == frames_per_launch
+                and str(t.get("kernel", "")).startswith(kernel_symbol + "<false")):  # counter-free build
+            return t
+    return {}
 
 
 def library_sha256() -> str:
@@ -450,17 +478,7 @@ def main():
         # §8(d)'s byte model: LOGICAL bytes per launch (every node / triangle / record read the algorithm makes,
         # whether L1/L2/Infinity Cache or HBM serves it) — a work measure, not a bound on this cache-resident kernel
         logical_per_launch = algorithmic_bytes(cnt) / launches if counters_ok else None
-        pmc = {}
-        tfile = ROOT / "profiles" / "pmc_traffic.json"
-        if tfile.exists():
-            try:
-                t = json.loads(tfile.read_text())
-                if (t.get("config") == args.config and t.get("width") == W and t.get("height") == H
-                        and t.get("frames_per_launch") == frames_per_step
-                        and str(t.get("kernel", "")).startswith(kernel_symbol + "<false")):  # counter-free build
-                    pmc = t
-            except Exception:
-                pmc = {}
+        pmc = committed_counters(args.config, W, H, frames_per_step, kernel_symbol)
         roofline = roofline_of(pmc, mean_launch_s, logical_per_launch, kernel_symbol,
                                dt / max(args.steps, 1) if launches == args.steps else 0.0)
         result = {

@@ -41,6 +41,11 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline")
     ap.add_argument("--library-sha256", default="", help="sha256 of the libhalogen_hip.so the profile ran")
+    ap.add_argument("--warmup-launches", type=int, default=2,
+                    help="launches of the production kernel before bench.py's timed region (its --warmup)")
+    ap.add_argument("--traffic-out", default="pmc_traffic.json",
+                    help="file under profiles/ for the production kernel's per-launch counters (bench.py reads "
+                         "pmc_traffic.json for the headline config, pmc_traffic_<config>.json for the others)")
     a = ap.parse_args()
     src = Path(a.src)
     out = ROOT / "profiles"
@@ -65,6 +70,10 @@ def main():
                 stats[k]["launch_ms"] = v
                 if len(v) > 1:
                     stats[k]["avg_ms_after_first"] = sum(v[1:]) / (len(v) - 1)
+                if len(v) > a.warmup_launches:
+                    # the launches of bench.py's timed region: what its HIP events average (roofline.mean_launch_ms)
+                    t = v[a.warmup_launches:]
+                    stats[k]["avg_ms_timed"] = sum(t) / len(t)
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     calls = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in sorted(glob.glob(str(src / f"{a.tag}_*" / "*_counter_collection.csv"))):
@@ -124,7 +133,7 @@ def main():
             t["l2_hit_rate"] = k["l2_hit_rate"]
         if "vmem_unit_busy" in k:
             t["vmem_unit_busy"] = k["vmem_unit_busy"]
-        (out / "pmc_traffic.json").write_text(json.dumps(t, indent=1) + "\n")
+        (out / a.traffic_out).write_text(json.dumps(t, indent=1) + "\n")
     print(json.dumps(summary, indent=1))
 
 
