@@ -105,8 +105,10 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     (`reps` steps; device sync on both sides):
       value       the library's default: consecutive calls are held and launched HG_OPT_COALESCE (32) frames at a time;
       strict      HG_OPT_COALESCE 1: every call its own launch (traces of consecutive launches overlap on two streams);
-      with_readback  the C# pass's per-frame hg_readback of the 33 MB image after every call (which launches the held
-                  frame, so this is one launch per frame too)."""
+      with_readback  hg_readback of the 33 MB image into a caller buffer after every call (which launches the held
+                  frame, so this is one launch per frame too);
+      with_display_readback  the C# pass's per-frame display path, hg_readback_begin/_end into the context's pinned
+                  images: "sync" shows frame k before tracing k+1, "pipelined" one frame behind."""
     def fresh():
         ctx.clear_accumulation()
         ctx.set_params(params)
@@ -146,6 +148,28 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         ctx.render(1, True)
         ctx.readback(W, H, img)
     dt_rb = time.perf_counter() - t1
+    # display readback through the context's pinned images (hg_readback_begin/_end): the image of this frame before the
+    # next is traced (sync), or one frame behind so that frame k's copy overlaps frame k+1's trace (pipelined)
+    display = {}
+    for mode in ("sync", "pipelined"):
+        fresh()
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        pending = 0
+        for _ in range(frames):
+            ctx.render(1, True)
+            ctx.readback_begin()
+            pending += 1
+            if mode == "sync" or pending == 2:
+                ctx.readback_end(W, H, copy=False)
+                pending -= 1
+        while pending:
+            ctx.readback_end(W, H, copy=False)
+            pending -= 1
+        dt_d = time.perf_counter() - t1
+        display[mode] = {"value": paths / dt_d / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_d * 1e3 / frames}
+    last = ctx.readback(W, H)
+    display["last_image_identical"] = bool(np.array_equal(batched.view(np.uint32), last.view(np.uint32)))
     ctx.set_option(abi.HG_OPT_COALESCE, 32)
     value = paths * reps / dt / 1e6
     strict = paths * reps / dt_s / 1e6
@@ -156,6 +180,7 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
                        "launches_per_step": c_s["launches"] / reps, "frac_of_batched": strict / batched_value},
             "with_readback": {"value": paths / dt_rb / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_rb * 1e3 / frames,
                               "readback_bytes_per_frame": W * H * 16},
+            "with_display_readback": display,
             "bit_identical_to_batched": identical}
 
 
@@ -253,7 +278,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=3)  # both trace streams sort a cost order before the timed launches
     ap.add_argument("--config", default="C3", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
@@ -350,6 +375,8 @@ def main():
     ctx.set_params(params)
     comm = None
     gather_mode = args.gather
+
+    os.environ.setdefault("HALOGEN_COMM_TIMEOUT_MS", "30000")  # hg_comm's deadline for a missing or failed peer
 
     def join_comm():  # hg_comm over RCCL: rank 0 makes the id, every rank joins (bounded by the comm deadline)
         box = [abi.comm_unique_id() if rank == 0 else None]

@@ -88,6 +88,8 @@ public static class HalogenNative
     [DllImport(Lib)] public static extern int hg_render(IntPtr ctx, int nFrames, int accumulate);
     [DllImport(Lib)] public static extern int hg_synchronize(IntPtr ctx);
     [DllImport(Lib)] public static extern int hg_readback(IntPtr ctx, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_readback_begin(IntPtr ctx);
+    [DllImport(Lib)] public static extern int hg_readback_end(IntPtr ctx, out IntPtr rgba, out UIntPtr nFloats);
     [DllImport(Lib)] public static extern int hg_set_accumulation(IntPtr ctx, float[] rgba, UIntPtr nFloats, int frameCount);
     [DllImport(Lib)] public static extern int hg_copy_tiles_device(IntPtr ctx, IntPtr dstDevice, UIntPtr nBytes);
     [DllImport(Lib)] public static extern int hg_local_tile_count(IntPtr ctx);

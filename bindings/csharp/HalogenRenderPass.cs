@@ -240,7 +240,14 @@ public class HalogenRenderPass : ScriptableRenderPass
         }
         else
         {
-            Check(HalogenNative.hg_readback(contexts[0], pixels, n), "hg_readback");
+            // one GPU: untiled on the device and copied into the context's pinned image, loaded from there
+            Check(HalogenNative.hg_readback_begin(contexts[0]), "hg_readback_begin");
+            Check(HalogenNative.hg_readback_end(contexts[0], out IntPtr image, out UIntPtr nImage), "hg_readback_end");
+            uploadTexture.LoadRawTextureData(image, checked((int)nImage.ToUInt64() * sizeof(float)));
+            uploadTexture.Apply(false);
+            Graphics.Blit(uploadTexture, rtDisplay);
+            haveImage = true;
+            return;
         }
         uploadTexture.SetPixelData(pixels, 0);
         uploadTexture.Apply(false);
@@ -371,5 +378,19 @@ public class HalogenRenderPass : ScriptableRenderPass
     public int getFrameCount()
     {
         return FrameCount;
+    }
+
+    // Checkpoint resume (not in the reference, whose resumable state is the accumulation target and FrameCount,
+    // RP:152,185,347): after OnCameraSetup at the image's size, Restore(image, frameCount, camera) continues the
+    // progressive render bit-identically (hg_set_accumulation; with several GPUs each context takes its own tiles).
+    // internal, so the public surface stays the reference's.
+    internal void Restore(float[] image, int frameCount, Transform cameraTransform)
+    {
+        foreach (IntPtr ctx in contexts)
+            Check(HalogenNative.hg_set_accumulation(ctx, image, (UIntPtr)image.Length, frameCount), "hg_set_accumulation");
+        FrameCount = frameCount;
+        AccumulationBufferDirty = false;
+        PriorCameraPosition = cameraTransform.position;  // the restored frames' camera: no restart on the next Execute
+        PriorCameraRotation = cameraTransform.rotation;
     }
 }

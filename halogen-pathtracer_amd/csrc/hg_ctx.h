@@ -89,6 +89,14 @@ struct hg_ctx {
     // same image; 1 = every call launches at once.
     int32_t coalesce = HG_COALESCE;
     int32_t pending_frames = 0, pending_acc = 0;
+
+    // Display readback (hg_readback, hg_readback_begin / _end): the accumulator untiled on the device into `image`
+    // (row-major float4), then copied into one of two pinned host images
+    DevBuf image;
+    float* image_host[2] = {nullptr, nullptr};
+    size_t image_host_bytes = 0;
+    hipEvent_t image_copied[2] = {nullptr, nullptr};
+    int rb_next = 0, rb_pending = 0;  // host image the next begin fills; begun readbacks not yet ended (<= 2)
 };
 
 // Launch the held frames of a context, if any (hg_runtime.hip; every entry point but hg_render calls it first)

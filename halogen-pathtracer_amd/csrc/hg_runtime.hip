@@ -19,6 +19,7 @@
 #include "hg_fmath.h"
 #include "hg_layout.h"
 #include "hg_ctx.h"
+#include "hg_tiling.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
@@ -309,6 +310,7 @@ int alloc_target(hg_ctx* c) {
 #else
     (void)slots;
 #endif
+    c->rb_pending = 0;  // quiesced: begun readbacks are complete, and their images die with the old size or tiling
     release(c->acc);
     if (bytes) {
         hipError_t e = hipMalloc(&c->acc.p, bytes);
@@ -456,6 +458,11 @@ void hg_destroy(hg_ctx* c) {
         if (L.traced) (void)hipEventDestroy(L.traced);
         if (L.blended) (void)hipEventDestroy(L.blended);
         if (L.stream) (void)hipStreamDestroy(L.stream);
+    }
+    release(c->image);
+    for (int k = 0; k < 2; ++k) {
+        if (c->image_host[k]) (void)hipHostFree(c->image_host[k]);
+        if (c->image_copied[k]) (void)hipEventDestroy(c->image_copied[k]);
     }
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
@@ -1030,7 +1037,80 @@ int hg_ctx_flush(hg_ctx* c) {
     return render_now(c, n, acc);
 }
 
+// The accumulator (this rank's tiles, tile-major) as a row-major image; pixels of other ranks' tiles are 0.  One thread
+// per pixel: the stores are contiguous, the loads are 8 consecutive float4 per tile row.
+__global__ __launch_bounds__(256) void hg_untile_image(float4* __restrict__ image, const float4* __restrict__ acc,
+                                                       int32_t W, int32_t H, int32_t tiles_x, int32_t rank,
+                                                       int32_t n_ranks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= uint32_t(W) * uint32_t(H)) return;
+    const HgPixelSource s = hg_pixel_source(i % uint32_t(W), i / uint32_t(W), uint32_t(tiles_x), uint32_t(n_ranks));
+    image[i] = s.rank == uint32_t(rank) ? acc[size_t(s.local_tile) * 64u + s.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+namespace {
+
+// Enqueue on the context stream: untile the accumulator into c->image (grown as needed).  Returns its size in bytes.
+int untile_async(hg_ctx* c, size_t* bytes) {
+    const size_t pixels = size_t(c->W) * size_t(c->H);
+    *bytes = pixels * sizeof(float4);
+    if (c->image.bytes < *bytes) {  // everything that might read the old image is ordered before on the context stream
+        HG_HIP(c, hipStreamSynchronize(c->stream));
+        if (int rc = ensure(c, c->image, *bytes)) return rc;
+    }
+    hipLaunchKernelGGL(hg_untile_image, dim3(uint32_t((pixels + 255) / 256)), dim3(256), 0, c->stream,
+                       static_cast<float4*>(c->image.p), static_cast<const float4*>(c->acc.p), c->W, c->H, c->tiles_x,
+                       c->rank, c->n_ranks);
+    HG_HIP(c, hipGetLastError());
+    return HG_OK;
+}
+
+}  // namespace
+
 extern "C" {
+
+int hg_readback_begin(hg_ctx* c) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
+    if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
+    if (c->rb_pending >= 2) return fail(c, HG_E_INVALID, "two readbacks outstanding: call hg_readback_end first");
+    if (int rc = set_device(c)) return rc;
+    size_t bytes = 0;
+    if (int rc = untile_async(c, &bytes)) return rc;
+    if (c->image_host_bytes != bytes) {  // (re)size both host images; none is outstanding (rb_pending counts them)
+        if (c->rb_pending) HG_HIP(c, hipStreamSynchronize(c->stream));
+        for (int k = 0; k < 2; ++k) {
+            if (c->image_host[k]) HG_HIP(c, hipHostFree(c->image_host[k]));
+            c->image_host[k] = nullptr;
+        }
+        c->image_host_bytes = 0;
+        for (int k = 0; k < 2; ++k) {
+            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->image_host[k]), bytes, 0);
+            if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+            if (!c->image_copied[k]) HG_HIP(c, hipEventCreateWithFlags(&c->image_copied[k], hipEventDisableTiming));
+        }
+        c->image_host_bytes = bytes;
+        c->rb_pending = 0;
+    }
+    const int k = c->rb_next;
+    HG_HIP(c, hipMemcpyAsync(c->image_host[k], c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HG_HIP(c, hipEventRecord(c->image_copied[k], c->stream));
+    c->rb_next = k ^ 1;
+    c->rb_pending++;
+    return HG_OK;
+}
+
+int hg_readback_end(hg_ctx* c, const float** rgba, size_t* n_floats) {
+    if (!c || !rgba) return HG_E_INVALID;
+    if (c->rb_pending <= 0) return fail(c, HG_E_INVALID, "no readback outstanding: call hg_readback_begin first");
+    if (int rc = set_device(c)) return rc;
+    const int k = c->rb_pending == 2 ? c->rb_next : c->rb_next ^ 1;  // the oldest begun
+    HG_HIP(c, hipEventSynchronize(c->image_copied[k]));
+    c->rb_pending--;
+    *rgba = c->image_host[k];
+    if (n_floats) *n_floats = c->image_host_bytes / sizeof(float);
+    return HG_OK;
+}
 
 int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (!c) return HG_E_INVALID;
@@ -1063,6 +1143,14 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
     if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
     if (n_floats < size_t(c->W) * size_t(c->H) * 4) return fail(c, HG_E_INVALID, "readback buffer too small");
     if (int rc = set_device(c)) return rc;
+    if (c->n_ranks == 1) {  // the whole image: untiled on the device, one copy into the caller's memory
+        size_t bytes = 0;
+        if (int rc = untile_async(c, &bytes)) return rc;
+        HG_HIP(c, hipMemcpyAsync(rgba, c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        HG_HIP(c, hipStreamSynchronize(c->stream));
+        return drain_events(c);
+    }
+    // this rank's pixels only (the others are left untouched): the tiles are repacked on the host
     std::vector<float4> tiles(size_t(c->n_local_tiles) * 64);
     if (!tiles.empty())
         HG_HIP(c, hipMemcpyAsync(tiles.data(), c->acc.p, tiles.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));

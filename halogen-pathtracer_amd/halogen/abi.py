@@ -101,7 +101,7 @@ HG_OPT_COALESCE = 9
 EXPORTS = [
     "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
-    "hg_readback", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
+    "hg_readback", "hg_readback_begin", "hg_readback_end", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
     "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
     "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_synchronize",
     "hg_comm_readback", "hg_comm_set_timeout_ms", "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
@@ -140,6 +140,8 @@ def lib() -> C.CDLL:
         "hg_render": (C.c_int, [P, i32, i32]),
         "hg_synchronize": (C.c_int, [P]),
         "hg_readback": (C.c_int, [P, f32p, sz]),
+        "hg_readback_begin": (C.c_int, [P]),
+        "hg_readback_end": (C.c_int, [P, C.POINTER(f32p), C.POINTER(sz)]),
         "hg_set_accumulation": (C.c_int, [P, f32p, sz, i32]),
         "hg_copy_tiles_device": (C.c_int, [P, P, sz]),
         "hg_local_tile_count": (i32, [P]),
@@ -262,6 +264,20 @@ class Context:
             out = np.zeros((h, w, 4), dtype=np.float32)
         self._check(lib().hg_readback(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size), "hg_readback")
         return out
+
+    def readback_begin(self) -> None:
+        """hg_readback_begin: enqueue the display readback of every frame rendered so far (at most 2 outstanding)."""
+        self._check(lib().hg_readback_begin(self._h), "hg_readback_begin")
+
+    def readback_end(self, w: int, h: int, copy: bool = True) -> np.ndarray:
+        """hg_readback_end: the (h, w, 4) image of the oldest begun readback.  copy=False returns a view of the
+        context's pinned host image, valid until the second readback_begin after the one it came from."""
+        ptr, n = C.POINTER(C.c_float)(), C.c_size_t(0)
+        self._check(lib().hg_readback_end(self._h, C.byref(ptr), C.byref(n)), "hg_readback_end")
+        if n.value != w * h * 4:
+            raise HalogenError(f"hg_readback_end: {n.value} floats for a {w}x{h} target")
+        view = np.ctypeslib.as_array(ptr, shape=(h, w, 4))
+        return view.copy() if copy else view
 
     def set_accumulation(self, image: np.ndarray, frame_count: int) -> None:
         """Checkpoint resume (hg_set_accumulation): the (h, w, 4) image hg_readback returned and the FrameCount of

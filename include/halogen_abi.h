@@ -253,6 +253,17 @@ int hg_synchronize(hg_ctx* ctx);
  * rank's pixels are written; the others are left untouched. Blocks. */
 int hg_readback(hg_ctx* ctx, float* rgba, size_t n_floats);
 
+/* Display readback, pipelined (the reference's per-frame Blit to rtCameraColor, RP:343-347, as a host image):
+ * hg_readback_begin enqueues, after every frame rendered so far, the untiling of the accumulation target into a
+ * row-major RGBA32F image and its copy into one of two pinned host images owned by the context, and returns at
+ * once; hg_readback_end waits for the OLDEST begun readback and hands out its image (width*height*4 floats; with
+ * tiling, other ranks' pixels are 0).  At most two readbacks are outstanding, so a caller can trace frame k+1 while
+ * frame k's image crosses PCIe:  render(1); begin; if (2 outstanding) end -> display.
+ * The pointer stays valid until the second hg_readback_begin after the one it came from, or until hg_resize /
+ * hg_set_tiling / hg_destroy.  hg_readback_end launches no held frames (hg_readback_begin already did). */
+int hg_readback_begin(hg_ctx* ctx);
+int hg_readback_end(hg_ctx* ctx, const float** rgba, size_t* n_floats);
+
 /* Checkpoint / resume: the inverse of hg_readback.  The reference's whole resumable state is the accumulation target
  * and FrameCount (RP:152, RP:185, RP:347).  Loads a row-major RGBA32F image (width*height*4 floats, as hg_readback
  * returns it; with tiling only this rank's pixels are read) into the accumulation target and sets the FrameCount the

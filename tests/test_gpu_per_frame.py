@@ -178,3 +178,60 @@ def test_gpu_set_accumulation_errors_are_loud(gpu):
             ctx.set_accumulation(np.zeros((32, 64, 4), np.float32), 1)
         with pytest.raises(abi.HalogenError, match="frame_count"):
             ctx.set_accumulation(np.zeros((64, 64, 4), np.float32), 0)
+
+
+@pytest.mark.gpu
+def test_gpu_display_readback_pipelined(gpu):
+    """hg_readback_begin/_end (the C# pass's display path): each frame's image equals the image of that many frames,
+    when taken at once (begin, end) and one frame behind (two outstanding); with a 3-way tiling the other ranks'
+    pixels read 0; misuse fails loudly; hg_resize drops the outstanding readbacks."""
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    want = [gpu_render(packed, params, k, True, cube)[0] for k in (1, 2, 3, 4, 5)]
+    with abi.Context(0) as ctx:
+        ctx.upload_scene(packed)
+        ctx.resize(W, H)
+        with pytest.raises(abi.HalogenError, match="no readback outstanding"):
+            ctx.readback_end(W, H)
+        ctx.set_params(params)
+        ctx.render(1, True)
+        ctx.readback_begin()
+        assert_bitwise(ctx.readback_end(W, H), want[0], "display readback, frame 1")
+        got = []
+        for k in range(1, 5):  # frames 2..5, one frame behind
+            ctx.render(1, True)
+            ctx.readback_begin()
+            if k >= 2 and k < 4:
+                got.append(ctx.readback_end(W, H))
+        with pytest.raises(abi.HalogenError, match="two readbacks outstanding"):  # frames 4 and 5 are
+            ctx.readback_begin()
+        got.append(ctx.readback_end(W, H))
+        got.append(ctx.readback_end(W, H))
+        for k, img in enumerate(got):
+            assert_bitwise(img, want[k + 1], f"pipelined display readback, frame {k + 2}")
+        with pytest.raises(abi.HalogenError, match="no readback outstanding"):
+            ctx.readback_end(W, H)
+
+
+@pytest.mark.gpu
+def test_gpu_display_readback_tiling_and_resize(gpu):
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    full, _ = gpu_render(packed, params, 2, True, cube)
+    own, _ = gpu_render(packed, params, 2, True, cube, tiling=(1, 3))  # other ranks' pixels NaN (left untouched)
+    with abi.Context(0) as ctx:
+        ctx.upload_scene(packed)
+        ctx.resize(W, H)
+        ctx.set_tiling(1, 3)
+        ctx.set_params(params)
+        ctx.render(2, True)
+        ctx.readback_begin()
+        img = ctx.readback_end(W, H, copy=False)
+        mine = ~np.isnan(own[..., 0])
+        assert mine.any() and (~mine).any()
+        assert_bitwise(img[mine], full[mine], "display readback, this rank's pixels")
+        assert not img[~mine].any(), "other ranks' pixels must read 0"
+        ctx.readback_begin()
+        ctx.resize(W // 2, H)  # drops the outstanding readback (and its image)
+        with pytest.raises(abi.HalogenError, match="no readback outstanding"):
+            ctx.readback_end(W // 2, H)
