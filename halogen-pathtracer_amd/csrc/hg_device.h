@@ -876,6 +876,61 @@ __device__ __forceinline__ void node_prefetch(const HgKernelParams& kp, uint32_t
 }
 #endif
 
+#if HG_QUAD_FETCH
+// Quad-cooperative node fetch (DESIGN.md §10 lever 4).  A descent step loads one 64-B record per lane with four 16-B
+// loads, each touching up to 64 records per wave instruction, and the texture data path prices an instruction by the
+// lines it touches.  Here the four lanes of each quad load their four records one after another (round j: lane q loads
+// quarter q of quad-lane j's record, so an instruction touches at most 16 records, each as one contiguous 64 B), and a
+// 4x4 transpose inside the quad (two DPP butterfly stages) hands every lane its own record: the same bytes, the same
+// result.  Every lane of the wave must take part (trav_step runs with the whole wave active).
+template <int kCtrl>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_mov_dpp(int(v), kCtrl, 0xF, 0xF, true));
+}
+template <int kCtrl>
+__device__ __forceinline__ float qpermf(float v) { return __uint_as_float(qperm<kCtrl>(__float_as_uint(v))); }
+// one butterfly stage over columns (a, b) = (j, j ^ s): a' = hi ? partner's b : a, b' = hi ? b : partner's a
+template <int kCtrl>
+__device__ __forceinline__ void quad_stage(float4& a, float4& b, bool hi) {
+    const float4 pa = make_float4(qpermf<kCtrl>(a.x), qpermf<kCtrl>(a.y), qpermf<kCtrl>(a.z), qpermf<kCtrl>(a.w));
+    const float4 pb = make_float4(qpermf<kCtrl>(b.x), qpermf<kCtrl>(b.y), qpermf<kCtrl>(b.z), qpermf<kCtrl>(b.w));
+    a = make_float4(hi ? pb.x : a.x, hi ? pb.y : a.y, hi ? pb.z : a.z, hi ? pb.w : a.w);
+    b = make_float4(hi ? b.x : pa.x, hi ? b.y : pa.y, hi ? b.z : pa.z, hi ? b.w : pa.w);
+}
+// The records of the lanes with `want` (others: unspecified); false = the caller loads per lane (adaptive mode chose
+// the per-lane path for this step)
+__device__ __forceinline__ bool quad_node_fetch(const HgKernelParams& kp, bool want, uint32_t node, float4& c0,
+                                                float4& c1, float4& c2, float4& c3) {
+    const uint32_t q = __lane_id() & 3u;
+    const uint32_t key = want ? node : HG_NONE;
+    const uint32_t k0 = qperm<0x00>(key), k1 = qperm<0x55>(key), k2 = qperm<0xAA>(key), k3 = qperm<0xFF>(key);
+#if HG_QUAD_FETCH == 2
+    // quads that need 2+ distinct records (where one full-record load per round beats four 64-record loads)
+    const bool spread = q == 0u && ((k1 != k0 && k1 != HG_NONE && k0 != HG_NONE) ||
+                                    (k2 != k0 && k2 != k1 && k2 != HG_NONE) ||
+                                    (k3 != k0 && k3 != k1 && k3 != k2 && k3 != HG_NONE));
+    if (wave_count(spread) < uint32_t(HG_QUAD_MIN)) return false;
+#endif
+    const uint32_t qo = q << 4;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
+    if (k0 != HG_NONE) r0 = ld_off(kp.nodes, (k0 << 6) + qo);
+    if (k1 != HG_NONE) r1 = ld_off(kp.nodes, (k1 << 6) + qo);
+    if (k2 != HG_NONE) r2 = ld_off(kp.nodes, (k2 << 6) + qo);
+    if (k3 != HG_NONE) r3 = ld_off(kp.nodes, (k3 << 6) + qo);
+    // r_j holds quarter q of quad-lane j's record; transpose so that lane q holds quarters 0..3 of its own
+    const bool h1 = (q & 1u) != 0u, h2 = (q & 2u) != 0u;
+    quad_stage<0xB1>(r0, r1, h1);  // quad_perm 1,0,3,2
+    quad_stage<0xB1>(r2, r3, h1);
+    quad_stage<0x4E>(r0, r2, h2);  // quad_perm 2,3,0,1
+    quad_stage<0x4E>(r1, r3, h2);
+    c0 = r0;
+    c1 = r1;
+    c2 = r2;
+    c3 = r3;
+    return true;
+}
+#endif
+
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
@@ -939,8 +994,23 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     uint64_t dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     while (dm != 0ull && (uint32_t(__builtin_popcountll(dm)) > dt || dm == act_mask)) {
         c.node_rounds += wave_once();
+#if HG_QUAD_FETCH && !HG_NODE_CACHE
+        const bool want = act && int32_t(t.node) >= 0;
+        float4 a_lo, a_hi, b_lo, b_hi;
+        const bool coop = quad_node_fetch(kp, want, t.node, a_lo, a_hi, b_lo, b_hi);
+        if (want) {
+            if (!coop) {
+                const uint32_t ro = t.node << 6;
+                a_lo = ld_off(kp.nodes, ro);
+                a_hi = ld_off(kp.nodes, ro + 16);
+                b_lo = ld_off(kp.nodes, ro + 32);
+                b_hi = ld_off(kp.nodes, ro + 48);
+            }
+#else
         if (act && int32_t(t.node) >= 0) {
-#if HG_NODE_CACHE
+#endif
+#if HG_QUAD_FETCH && !HG_NODE_CACHE
+#elif HG_NODE_CACHE
             // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
             float4 a_lo, a_hi, b_lo, b_hi;
             if (t.node < kp.hot_records) {

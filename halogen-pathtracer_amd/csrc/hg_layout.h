@@ -110,6 +110,12 @@
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
+#ifndef HG_QUAD_FETCH
+#define HG_QUAD_FETCH 0  // streaming traversal node fetch: 1 = quad-cooperative (each quad loads its 4 lanes' records
+#endif                   // whole, one record per round, then a DPP transpose), 2 = cooperative only when >= HG_QUAD_MIN
+#ifndef HG_QUAD_MIN      // of the 16 quads need 2+ distinct records (DESIGN.md §10 lever 4)
+#define HG_QUAD_MIN 8
+#endif
 #ifndef HG_TILE_ORDER
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif
