@@ -230,6 +230,26 @@ __device__ __forceinline__ size_t fc_slot_frame(size_t slot, uint32_t f, size_t 
     return size_t(f) * n_slots + slot;
 #endif
 }
+// Frame colours are written once by the trace and read once by the blend: with HG_FC_NT both go through the
+// non-temporal hint, so the 2.1 GB a 64-frame C3 launch writes is not kept in L2 ahead of the BVH lines
+__device__ __forceinline__ void fc_store(float4* p, float4 v) {
+#if HG_FC_NT
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ float4 fc_load(const float4* p) {
+#if HG_FC_NT
+    return make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
+                       __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
+#else
+    return *p;
+#endif
+}
 __device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f, size_t slot) {
     return fc_slot_frame(slot, f, size_t(uint32_t(kp.n_local_tiles)) * 64u, uint32_t(kp.n_frames));
 }

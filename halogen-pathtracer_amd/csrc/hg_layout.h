@@ -110,6 +110,9 @@
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
+#ifndef HG_FC_NT
+#define HG_FC_NT 1  // frame-colour stores (trace) and loads (blend) with the non-temporal hint (+0.2..0.6 %, sweep_r03_n)
+#endif
 #ifndef HG_QUAD_FETCH
 #define HG_QUAD_FETCH 0  // streaming traversal node fetch: 1 = quad-cooperative (each quad loads its 4 lanes' records
 #endif                   // whole, one record per round, then a DPP transpose), 2 = cooperative only when >= HG_QUAD_MIN

@@ -419,8 +419,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
                     if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
-                        kp.frame_color[fc_index(kp, fs >> 16, slot_i)] =
-                            make_float4(color.x, color.y, color.z, 1.0f);
+                        fc_store(kp.frame_color + fc_index(kp, fs >> 16, slot_i),
+                                 make_float4(color.x, color.y, color.z, 1.0f));
                     } else {
                         float4* slot = kp.acc + slot_i;
                         float4 acc = *slot;
@@ -517,9 +517,9 @@ __global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc,
     float4 a = acc[i];
     for (int32_t f = 0; f < n_frames; ++f) {
 #if HG_FC_SLOT_MAJOR
-        const float4 c = colors[size_t(i) * uint32_t(n_frames) + uint32_t(f)];  // fc_index (hg_device.h)
+        const float4 c = fc_load(colors + size_t(i) * uint32_t(n_frames) + uint32_t(f));  // fc_index (hg_device.h)
 #else
-        const float4 c = colors[size_t(f) * n_slots + i];
+        const float4 c = fc_load(colors + size_t(f) * n_slots + i);
 #endif
         if (accumulate) {
             const float w = rcp_exact(float(uint32_t(first_frame + f)));
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ a
 #pragma unroll
         for (uint32_t r = 0; r < 8u; ++r) {
             const uint32_t j = lane + 64u * r, s = j >> 3, ff = j & 7u;
-            if (f0 + ff < nf) st[s * kRow + ff] = colors[size_t(slot0 + s) * nf + f0 + ff];
+            if (f0 + ff < nf) st[s * kRow + ff] = fc_load(colors + size_t(slot0 + s) * nf + f0 + ff);
         }
         wave_lds_sync();
         const uint32_t fe = nf - f0 < 8u ? nf - f0 : 8u;
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(64) void hg_blend_frames_lean(float4* __restrict__ 
     if (i >= n_slots) return;
     float4 a = acc[i];
     for (int32_t f = 0; f < n_frames; ++f) {
-        const float4 c = colors[fc_slot_frame(i, uint32_t(f), n_slots, uint32_t(n_frames))];
+        const float4 c = fc_load(colors + fc_slot_frame(i, uint32_t(f), n_slots, uint32_t(n_frames)));
         if (accumulate) {
             const float w = rcp_exact(float(uint32_t(first_frame + f)));
             const float k = 1.0f - w;
@@ -965,7 +965,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     const size_t slot_i = kQueue ? size_t(slot) : size_t(uint32_t(local_tile)) * 64u + pix;
                     // this frame's colour, blended later in frame order (hg_blend_frames)
 #if !HG_DIAG_NO_FC  // (analysis builds only: the write-traffic attribution of DESIGN.md §4.5)
-                    if (!fresh) kp.frame_color[fc_index(kp, fs >> 16, slot_i)] = make_float4(color.x, color.y, color.z, 1.0f);
+                    if (!fresh)
+                        fc_store(kp.frame_color + fc_index(kp, fs >> 16, slot_i), make_float4(color.x, color.y, color.z, 1.0f));
 #endif
                     fs = (fs & 0xFFFF0000u) + 0x10000u;
                     if constexpr (kQueue) {
