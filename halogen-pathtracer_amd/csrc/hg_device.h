@@ -255,7 +255,8 @@ __device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f,
 }
 
 // Triangle ti's Moller-Trumbore operands from the three SoA streams: a = (v0, e1.x), b = (e1.yz, e2.xy), cz = e2.z.
-// (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md.)
+// (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md;
+// the non-temporal hint on these loads: C3 -9.7 %, C3F -10 %, tools/sweeps/sweep_r03_o.jsonl.)
 __device__ __forceinline__ void tri_load(const HgKernelParams& kp, uint32_t ti, float4& a, float4& b, float& cz) {
     a = ld_off(kp.tri_a, ti << 4);
     b = ld_off(kp.tri_b, ti << 4);
