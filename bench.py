@@ -87,10 +87,10 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)
     paths = W * H * frames_per_step * steps
     kernel_symbol = KERNEL_SYMBOL.get(int(c["last_kernel"]), "?")
-    mean_launch_s = timing["trace_ms"] / max(timing["trace_launches"], 1) / 1e3
+    mean_launch_s, span_s = launch_seconds(timing)
     # its own roofline, from the committed C3F PMC pass (profiles/pmc_traffic_C3F.json)
     roofline = roofline_of(committed_counters("C3F", W, H, frames_per_step, kernel_symbol), mean_launch_s,
-                           algorithmic_bytes(c), kernel_symbol, dt / steps)
+                           algorithmic_bytes(c), kernel_symbol, dt / steps, span_s)
     return {"workload": cfg.name, "value": paths / dt / 1e6, "unit": "Mpaths/s", "steps": steps,
             "ms_per_step": dt * 1e3 / steps, "mrays_per_s": c["rays"] / c["paths"] * paths / dt / 1e6,
             "primary_miss_frac": c["primary_misses"] / c["paths"], "rays_per_path": c["rays"] / c["paths"],
@@ -112,6 +112,8 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     def fresh():
         ctx.clear_accumulation()
         ctx.set_params(params)
+
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # the timed kernels (the counting replay before this leg turns them on)
 
     def timed(coalesce: int):
         ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
@@ -209,7 +211,18 @@ def library_sha256() -> str:
     return hashlib.sha256(abi.LIB_PATH.read_bytes()).hexdigest()
 
 
-def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str, step_s: float = 0.0) -> dict:
+def launch_seconds(timing: dict) -> tuple:
+    """(device time per trace launch, mean of the launches' own event spans).  Consecutive launches run on two trace
+    streams and overlap, so each launch's span also counts the time it shared the GPU with its neighbour; the union of
+    the spans (hg_counters.trace_busy_ms) per launch is the kernel's device time per launch, the roofline's divisor.
+    rocprofv3's kernel trace gives both (tools/summarize_profile.py: avg_ms_timed_union, avg_ms_timed)."""
+    n = max(timing.get("trace_launches", 0), 1)
+    busy = timing.get("trace_busy_ms", 0.0) or timing.get("trace_ms", 0.0)
+    return busy / n / 1e3, timing.get("trace_ms", 0.0) / n / 1e3
+
+
+def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str, step_s: float = 0.0,
+                events_launch_s: float = 0.0) -> dict:
     """The dominant kernel against what bounds it.  The trace kernel works on a cache-resident scene (C3: 90 MB,
     inside the 256 MiB Infinity Cache) and is bound by VALU issue and latency, not HBM: `frac` is its VALU issue rate
     (wave-level VALU instructions per launch, SQ_INSTS_VALU from the committed rocprofv3 pass of this workload and
@@ -239,6 +252,9 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "logical_bytes_per_launch": logical_per_launch,
             "logical_gbs": logical_per_launch / mean_launch_s / 1e9 if logical_per_launch and ok else None,
             "mean_launch_ms": mean_launch_s * 1e3, "kernel": kernel_symbol,
+            "launch_ms_basis": "union of the timed launches' HIP-event spans on both trace streams / launches",
+            "mean_launch_span_ms": events_launch_s * 1e3 if events_launch_s else None,
+            "frac_per_launch_span": valu / events_launch_s / 1e9 / VALU_PEAK_GINST if valu and events_launch_s else None,
             # launches of consecutive steps overlap (two trace streams): the step period is the throughput's clock
             "step_period_ms": step_s * 1e3 if step_s else None,
             "frac_per_step_period": valu / step_s / 1e9 / VALU_PEAK_GINST if valu and step_s else None,
@@ -477,7 +493,7 @@ def main():
         if timed_img is not None:
             replay_identical = bool(np.array_equal(timed_img.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
     cnt = ctx.counters()
-    for k in ("kernel_ms", "launches", "trace_ms", "trace_launches"):
+    for k in ("kernel_ms", "launches", "trace_ms", "trace_launches", "trace_busy_ms"):
         cnt[k] = timing[k]
     if dist is not None:
         import torch
@@ -499,15 +515,17 @@ def main():
     if rank == 0:
         launches = max(cnt["launches"], 1)
         # the trace kernel's own launch duration (events on its stream; what rocprofv3 --stats averages)
-        mean_launch_s = (cnt["trace_ms"] / cnt["trace_launches"] if cnt.get("trace_launches") else
-                         cnt["kernel_ms"] / launches) / 1e3
+        if cnt.get("trace_launches"):
+            mean_launch_s, span_s = launch_seconds(cnt)
+        else:
+            mean_launch_s, span_s = cnt["kernel_ms"] / launches / 1e3, 0.0
         counters_ok = not args.no_counters and cnt["paths"] > 0
         # §8(d)'s byte model: LOGICAL bytes per launch (every node / triangle / record read the algorithm makes,
         # whether L1/L2/Infinity Cache or HBM serves it) — a work measure, not a bound on this cache-resident kernel
         logical_per_launch = algorithmic_bytes(cnt) / launches if counters_ok else None
         pmc = committed_counters(args.config, W, H, frames_per_step, kernel_symbol)
         roofline = roofline_of(pmc, mean_launch_s, logical_per_launch, kernel_symbol,
-                               dt / max(args.steps, 1) if launches == args.steps else 0.0)
+                               dt / max(args.steps, 1) if launches == args.steps else 0.0, span_s)
         result = {
             "metric": METRIC,
             "value": total_paths / dt / 1e6,
@@ -554,7 +572,8 @@ def main():
             "abi_gather_check": abi_check,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
-                          "trace_total": cnt["trace_ms"], "trace_launches": cnt["trace_launches"]},
+                          "trace_total": cnt["trace_ms"], "trace_busy": cnt.get("trace_busy_ms"),
+                          "trace_launches": cnt["trace_launches"]},
             "cpu_baseline": None,
         }
         if args.save_image:

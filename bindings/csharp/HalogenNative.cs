@@ -61,6 +61,7 @@ public static class HalogenNative
         public ulong shade_rounds;
         public ulong primary_misses;
         public ulong exec_fallbacks;
+        public double trace_busy_ms;
     }
 
     public const int HG_OK = 0;

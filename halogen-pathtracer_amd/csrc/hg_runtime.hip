@@ -236,13 +236,32 @@ int drain_events(hg_ctx* c) {
         c->counters.kernel_ms += double(ms);
         c->free_events.push_back(pr);
     }
+    // the launches' intervals relative to the first start (the trace streams' events share the device clock); the
+    // batch ends at a synchronisation, so batches do not overlap one another
+    std::vector<std::pair<double, double>> iv;
+    iv.reserve(c->pending_trace.size());
     for (auto& pr : c->pending_trace) {
-        float ms = 0.0f;
+        float ms = 0.0f, a = 0.0f;
         HG_HIP(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+        HG_HIP(c, hipEventElapsedTime(&a, c->pending_trace.front().first, pr.first));
+        iv.emplace_back(double(a), double(a) + double(ms));
         c->counters.trace_ms += double(ms);
         c->counters.trace_launches++;
-        c->free_events.push_back(pr);
     }
+    std::sort(iv.begin(), iv.end());
+    double covered = 0.0, lo = 0.0, hi = -1.0;
+    for (const auto& x : iv) {
+        if (x.first > hi) {
+            if (hi > lo) covered += hi - lo;
+            lo = x.first;
+            hi = x.second;
+        } else if (x.second > hi) {
+            hi = x.second;
+        }
+    }
+    if (hi > lo) covered += hi - lo;
+    c->counters.trace_busy_ms += covered;
+    for (auto& pr : c->pending_trace) c->free_events.push_back(pr);
     c->pending.clear();
     c->pending_trace.clear();
     return HG_OK;

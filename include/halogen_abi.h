@@ -159,6 +159,9 @@ typedef struct hg_counters {
     uint64_t exec_fallbacks; /* HG_CHECK_EXEC builds only (hg_selftest HG_SELFTEST_BUILD): lane-events where the
                                 distributed leaf test found a lane of its wave inactive and took the sequential leaf
                                 loop; must stay 0 (its DPP scans need a full wave).  0 in product builds */
+    double trace_busy_ms;  /* the union of the traversal kernel's timed launch intervals (HG_OPT_TIMING): launches on the
+                              two trace streams overlap, so trace_ms counts shared time twice; trace_busy_ms /
+                              trace_launches is the kernel's device time per launch */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;

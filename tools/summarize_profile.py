@@ -63,8 +63,11 @@ def main():
     trace_csv = src / f"{a.tag}_stats" / "stats_kernel_trace.csv"
     if trace_csv.exists():
         durs = collections.defaultdict(list)
+        spans = collections.defaultdict(list)
         for r in csv.DictReader(open(trace_csv)):
-            durs[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            durs[kname(r["Kernel_Name"])].append((t1 - t0) / 1e6)
+            spans[kname(r["Kernel_Name"])].append((t0, t1))
         for k, v in durs.items():
             if k in stats:
                 stats[k]["launch_ms"] = v
@@ -74,6 +77,20 @@ def main():
                     # the launches of bench.py's timed region: what its HIP events average (roofline.mean_launch_ms)
                     t = v[a.warmup_launches:]
                     stats[k]["avg_ms_timed"] = sum(t) / len(t)
+                    # launches on the two trace streams overlap: the union of their intervals per launch is the
+                    # kernel's device time per launch (bench.py: trace_busy_ms / trace_launches)
+                    iv = sorted(spans[k][a.warmup_launches:])
+                    busy, lo, hi = 0, None, None
+                    for x0, x1 in iv:
+                        if hi is None or x0 > hi:
+                            if hi is not None:
+                                busy += hi - lo
+                            lo, hi = x0, x1
+                        else:
+                            hi = max(hi, x1)
+                    if hi is not None:
+                        busy += hi - lo
+                    stats[k]["avg_ms_timed_union"] = busy / 1e6 / len(iv)
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     calls = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in sorted(glob.glob(str(src / f"{a.tag}_*" / "*_counter_collection.csv"))):
