@@ -1,0 +1,49 @@
+"""The bench line's launch basis: consecutive trace launches overlap on two streams, so the roofline
+divides by the union of the timed launches' spans per launch, from the library's HIP events (hg_counters.trace_busy_ms,
+read through bench.launch_seconds) and from rocprofv3's kernel trace (tools/summarize_profile.interval_union)."""
+import importlib.util
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="module")
+def summ():
+    return _load("summarize_profile", ROOT / "tools" / "summarize_profile.py")
+
+
+@pytest.fixture(scope="module")
+def bench():
+    sys.path.insert(0, str(ROOT))
+    return _load("bench_mod", ROOT / "bench.py")
+
+
+def test_interval_union(summ):
+    u = summ.interval_union
+    assert u([]) == 0
+    assert u([(0, 10)]) == 10
+    assert u([(0, 10), (20, 30)]) == 20  # disjoint
+    assert u([(0, 10), (5, 15)]) == 15  # overlapping neighbours (two trace streams)
+    assert u([(5, 15), (0, 10), (12, 14)]) == 15  # unsorted, nested
+    assert u([(0, 10), (10, 20)]) == 20  # touching
+    # steady pipeline: launches of 48 starting every 38 units -> the union per launch tends to the period
+    spans = [(38 * k, 38 * k + 48) for k in range(100)]
+    assert u(spans) / len(spans) == pytest.approx(38.1)
+
+
+def test_launch_seconds(bench):
+    busy, span = bench.launch_seconds({"trace_busy_ms": 387.0, "trace_ms": 485.0, "trace_launches": 10})
+    assert busy == pytest.approx(0.0387) and span == pytest.approx(0.0485)
+    # a library without the union counter falls back to the span mean
+    busy, span = bench.launch_seconds({"trace_ms": 485.0, "trace_launches": 10})
+    assert busy == pytest.approx(0.0485) == span

@@ -31,6 +31,21 @@ def kname(raw: str) -> str:
     return raw.replace("void ", "").split("(")[0]
 
 
+def interval_union(spans) -> float:
+    """Total length covered by the (start, end) intervals (the time at least one of them runs)."""
+    busy, lo, hi = 0, None, None
+    for x0, x1 in sorted(spans):
+        if hi is None or x0 > hi:
+            if hi is not None:
+                busy += hi - lo
+            lo, hi = x0, x1
+        else:
+            hi = max(hi, x1)
+    if hi is not None:
+        busy += hi - lo
+    return busy
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
@@ -79,18 +94,8 @@ def main():
                     stats[k]["avg_ms_timed"] = sum(t) / len(t)
                     # launches on the two trace streams overlap: the union of their intervals per launch is the
                     # kernel's device time per launch (bench.py: trace_busy_ms / trace_launches)
-                    iv = sorted(spans[k][a.warmup_launches:])
-                    busy, lo, hi = 0, None, None
-                    for x0, x1 in iv:
-                        if hi is None or x0 > hi:
-                            if hi is not None:
-                                busy += hi - lo
-                            lo, hi = x0, x1
-                        else:
-                            hi = max(hi, x1)
-                    if hi is not None:
-                        busy += hi - lo
-                    stats[k]["avg_ms_timed_union"] = busy / 1e6 / len(iv)
+                    iv = spans[k][a.warmup_launches:]
+                    stats[k]["avg_ms_timed_union"] = interval_union(iv) / 1e6 / len(iv)
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     calls = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in sorted(glob.glob(str(src / f"{a.tag}_*" / "*_counter_collection.csv"))):
