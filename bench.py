@@ -67,7 +67,8 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)
     ctx.clear_accumulation()
     ctx.set_params(params)
-    ctx.render(frames_per_step, True)  # warm-up: records this view's tile costs for the cost order
+    for _ in range(2):  # warm-up, one launch per trace stream: each records this view's tile costs for its cost order
+        ctx.render(frames_per_step, True)
     ctx.clear_accumulation()
     ctx.set_params(params)
     ctx.synchronize()
