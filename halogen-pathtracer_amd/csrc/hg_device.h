@@ -291,6 +291,58 @@ __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-2
     return tMax > fmaxf(0.0f, tMin) ? tMin : HG_INF;
 }
 
+// A child-pair record (hg_runtime.hip, BLAS pass 2): both children's boxes and refs in 64 B, 56 of them used.
+// HG_PAIR_SOA lays the boxes out coordinate by coordinate with A and B side by side, so that the two box tests of a
+// descent step run on packed FP32 pairs (v_pk_add_f32 / v_pk_mul_f32: two IEEE operations per instruction, the same
+// results as the scalar ones):
+//   q0 = (A.lo.x, B.lo.x, A.lo.y, B.lo.y), q1 = (A.lo.z, B.lo.z, A.hi.x, B.hi.x), q2 = (A.hi.y, B.hi.y, A.hi.z, B.hi.z),
+//   q3 = (refA, refB, -, -);
+// otherwise q0 = (A.lo, refA), q1 = (A.hi, refB), q2 = (B.lo, -), q3 = (B.hi, -).
+struct NodePair {
+    float4 q0, q1, q2, q3;
+};
+__device__ __forceinline__ NodePair node_pair(const HgKernelParams& kp, uint32_t node) {
+    const uint32_t ro = node << 6;
+#if HG_PAIR_SOA
+    const uint2 refs = ld_off(reinterpret_cast<const uint2*>(kp.nodes), ro + 48);
+    return NodePair{ld_off(kp.nodes, ro), ld_off(kp.nodes, ro + 16), ld_off(kp.nodes, ro + 32),
+                    make_float4(__uint_as_float(refs.x), __uint_as_float(refs.y), 0.0f, 0.0f)};
+#else
+    return NodePair{ld_off(kp.nodes, ro), ld_off(kp.nodes, ro + 16), ld_off(kp.nodes, ro + 32), ld_off(kp.nodes, ro + 48)};
+#endif
+}
+__device__ __forceinline__ NodePair node_pair_at(const float4* p) { return NodePair{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ uint32_t pair_ref_a(const NodePair& r) {
+    return __float_as_uint(HG_PAIR_SOA ? r.q3.x : r.q0.w);
+}
+__device__ __forceinline__ uint32_t pair_ref_b(const NodePair& r) {
+    return __float_as_uint(HG_PAIR_SOA ? r.q3.y : r.q1.w);
+}
+// ray_aabb (:244-259) of both children: dA, dB
+__device__ __forceinline__ void pair_dist(const NodePair& r, f3 o, f3 inv, float& dA, float& dB) {
+#if HG_PAIR_SOA
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const v2f lx = (v2f{r.q0.x, r.q0.y} - o.x) * inv.x, ly = (v2f{r.q0.z, r.q0.w} - o.y) * inv.y;
+    const v2f lz = (v2f{r.q1.x, r.q1.y} - o.z) * inv.z, hx = (v2f{r.q1.z, r.q1.w} - o.x) * inv.x;
+    const v2f hy = (v2f{r.q2.x, r.q2.y} - o.y) * inv.y, hz = (v2f{r.q2.z, r.q2.w} - o.z) * inv.z;
+    float aMin = fminf(lx.x, hx.x), aMax = fmaxf(lx.x, hx.x);
+    aMin = fmaxf(aMin, fminf(ly.x, hy.x));
+    aMax = fminf(aMax, fmaxf(ly.x, hy.x));
+    aMin = fmaxf(aMin, fminf(lz.x, hz.x));
+    aMax = fminf(aMax, fmaxf(lz.x, hz.x));
+    float bMin = fminf(lx.y, hx.y), bMax = fmaxf(lx.y, hx.y);
+    bMin = fmaxf(bMin, fminf(ly.y, hy.y));
+    bMax = fminf(bMax, fmaxf(ly.y, hy.y));
+    bMin = fmaxf(bMin, fminf(lz.y, hz.y));
+    bMax = fminf(bMax, fmaxf(lz.y, hz.y));
+    dA = aMax > fmaxf(0.0f, aMin) ? aMin : HG_INF;
+    dB = bMax > fmaxf(0.0f, bMin) ? bMin : HG_INF;
+#else
+    dA = ray_aabb(xyz(r.q0), xyz(r.q1), o, inv);
+    dB = ray_aabb(xyz(r.q2), xyz(r.q3), o, inv);
+#endif
+}
+
 // Returns the closest accepted sphere as index | (orientation < 0) << 31 (HG_NONE if none), its distance in t;
 // position/normal/material are resolved after the mesh pass (resolve_sphere), with the same arithmetic.
 __device__ uint32_t isect_spheres(const HgKernelParams& kp, const Ray& ray, float& t) {  // :357-376
@@ -705,13 +757,11 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             c.node_rounds += wave_once();
             if (active && int32_t(node) >= 0) {
 #endif
-                const uint32_t ro = node << 6;
-                const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
-                             b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
-                const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
-                const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                const NodePair np = node_pair(kp, node);
+                float dA, dB;
+                pair_dist(np, lo, inv, dA, dB);
                 c.aabb += 2;
-                const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
                 // reference (:430-444): push far, push near (each only if tEntry < closest), pop near
                 const bool bFirst = dB < dA;
                 const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
@@ -796,13 +846,11 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
         while (__any(active)) {
             while (__any(active && !(node & HG_LEAF_BIT))) {
                 if (active && !(node & HG_LEAF_BIT)) {
-                    const uint32_t ro = node << 6;
-                    const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
-                                 b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
-                    const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
-                    const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                    const NodePair np = node_pair(kp, node);
+                    float dA, dB;
+                    pair_dist(np, lo, inv, dA, dB);
                     c.aabb += 2;
-                    const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                    const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
                     // reference (:430-444): push far, push near (each only if tEntry < closest), pop near
                     const bool bFirst = dB < dA;
                     const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
@@ -1017,49 +1065,31 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         c.node_rounds += wave_once();
 #if HG_QUAD_FETCH && !HG_NODE_CACHE
         const bool want = act && int32_t(t.node) >= 0;
-        float4 a_lo, a_hi, b_lo, b_hi;
-        const bool coop = quad_node_fetch(kp, want, t.node, a_lo, a_hi, b_lo, b_hi);
+        NodePair np;
+        const bool coop = quad_node_fetch(kp, want, t.node, np.q0, np.q1, np.q2, np.q3);
         if (want) {
-            if (!coop) {
-                const uint32_t ro = t.node << 6;
-                a_lo = ld_off(kp.nodes, ro);
-                a_hi = ld_off(kp.nodes, ro + 16);
-                b_lo = ld_off(kp.nodes, ro + 32);
-                b_hi = ld_off(kp.nodes, ro + 48);
-            }
+            if (!coop) np = node_pair(kp, t.node);
 #else
         if (act && int32_t(t.node) >= 0) {
 #endif
 #if HG_QUAD_FETCH && !HG_NODE_CACHE
 #elif HG_NODE_CACHE
             // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
-            float4 a_lo, a_hi, b_lo, b_hi;
-            if (t.node < kp.hot_records) {
-                const float4* cr = reinterpret_cast<const float4*>(hg_lds_stack + HG_STREAM_CACHE_ROW * 64u) + 4u * t.node;
-                a_lo = cr[0];
-                a_hi = cr[1];
-                b_lo = cr[2];
-                b_hi = cr[3];
-            } else {
-                const uint32_t ro = t.node << 6;
-                a_lo = ld_off(kp.nodes, ro);
-                a_hi = ld_off(kp.nodes, ro + 16);
-                b_lo = ld_off(kp.nodes, ro + 32);
-                b_hi = ld_off(kp.nodes, ro + 48);
-            }
+            const NodePair np = t.node < kp.hot_records
+                                    ? node_pair_at(reinterpret_cast<const float4*>(hg_lds_stack + HG_STREAM_CACHE_ROW * 64u) +
+                                                   4u * t.node)
+                                    : node_pair(kp, t.node);
 #else
-            const uint32_t ro = t.node << 6;
-            const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
-                         b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
+            const NodePair np = node_pair(kp, t.node);
 #endif
-            const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+            const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
 #if HG_NODE_PREFETCH
             // after all four loads have landed (vmcnt retires in order: a wait for a later load would include it)
-            asm volatile("" : : "v"(a_lo.w), "v"(a_hi.w), "v"(b_lo.z), "v"(b_hi.z));
+            asm volatile("" : : "v"(np.q0.w), "v"(np.q1.w), "v"(np.q2.z), "v"(np.q3.y));
             node_prefetch(kp, refA, refB);
 #endif
-            const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), t.lo, inv);
-            const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), t.lo, inv);
+            float dA, dB;
+            pair_dist(np, t.lo, inv, dA, dB);
             c.aabb += 2;
             const bool bFirst = dB < dA;  // :430-444
             const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;

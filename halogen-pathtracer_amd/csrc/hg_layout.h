@@ -110,6 +110,9 @@
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
+#ifndef HG_PAIR_SOA
+#define HG_PAIR_SOA 0  // child-pair records coordinate by coordinate, A and B side by side: packed-FP32 box tests
+#endif             // (node_pair / pair_dist in hg_device.h; the record writer in hg_runtime.hip)
 #ifndef HG_FC_NT
 #define HG_FC_NT 1  // frame-colour stores (trace) and loads (blend) with the non-temporal hint (+0.2..0.6 %, sweep_r03_n)
 #endif

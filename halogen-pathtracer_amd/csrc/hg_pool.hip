@@ -181,13 +181,11 @@ __global__ __launch_bounds__(64, HG_POOL_WAVES) void hg_trace_pool_kernel(const 
                     if (n_desc <= kp.descent_t && n_desc != uint32_t(__popcll(__ballot(act)))) break;
                     c.node_rounds += wave_once();
                     if (act && !(node & HG_LEAF_BIT)) {
-                        const uint32_t ro = node << 6;
-                        const float4 a_lo = ld_off(kp.nodes, ro), a_hi = ld_off(kp.nodes, ro + 16),
-                                     b_lo = ld_off(kp.nodes, ro + 32), b_hi = ld_off(kp.nodes, ro + 48);
-                        const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
-                        const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                        const NodePair np = node_pair(kp, node);
+                        float dA, dB;
+                        pair_dist(np, lo, inv, dA, dB);
                         c.aabb += 2;
-                        const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                        const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
                         const bool bFirst = dB < dA;  // :430-444
                         const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
                         const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;

@@ -186,6 +186,28 @@ uint32_t ubits(float f) {
     return u;
 }
 
+// The child-pair record layout (hg_device.h node_pair): where child 0 / 1's ref lives, and the writer
+float& pair_ref_slot(float4* r, int child) {
+#if HG_PAIR_SOA
+    return child == 0 ? r[3].x : r[3].y;
+#else
+    return child == 0 ? r[0].w : r[1].w;
+#endif
+}
+void put_pair(float4* r, const BVHEntry& A, const BVHEntry& B, uint32_t ra, uint32_t rb) {
+#if HG_PAIR_SOA
+    r[0] = f4(A.boundingCornerA.x, B.boundingCornerA.x, A.boundingCornerA.y, B.boundingCornerA.y);
+    r[1] = f4(A.boundingCornerA.z, B.boundingCornerA.z, A.boundingCornerB.x, B.boundingCornerB.x);
+    r[2] = f4(A.boundingCornerB.y, B.boundingCornerB.y, A.boundingCornerB.z, B.boundingCornerB.z);
+    r[3] = f4(bits(ra), bits(rb), 0.0f, 0.0f);
+#else
+    r[0] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z, bits(ra));
+    r[1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z, bits(rb));
+    r[2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
+    r[3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
+#endif
+}
+
 uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32_t k) {
     const uint32_t n = uint32_t(rec.size() / 4);
     k = std::min(k, n);
@@ -201,7 +223,7 @@ uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32
     for (size_t q = 0; q < queue.size() && next < k; ++q) {
         const uint32_t r = queue[q];
         for (int child = 0; child < 2 && next < k; ++child) {
-            const uint32_t ref = ubits(child == 0 ? rec[4 * size_t(r)].w : rec[4 * size_t(r) + 1].w);
+            const uint32_t ref = ubits(pair_ref_slot(&rec[4 * size_t(r)], child));
             if ((ref & HG_LEAF_BIT) || ref >= n || newi[ref] != HG_NONE) continue;
             newi[ref] = next++;
             queue.push_back(ref);
@@ -219,8 +241,8 @@ uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32
         dst[1] = src[1];
         dst[2] = src[2];
         dst[3] = src[3];
-        dst[0].w = bits(remap(ubits(src[0].w)));
-        dst[1].w = bits(remap(ubits(src[1].w)));
+        for (int child = 0; child < 2; ++child)
+            pair_ref_slot(dst, child) = bits(remap(ubits(pair_ref_slot(const_cast<float4*>(src), child))));
     }
     rec.swap(out);
     for (HgDevMesh& m : dm) m.root_ref = remap(m.root_ref);
@@ -637,11 +659,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
             if (expand.size() == mark + 2) std::swap(expand[mark], expand[mark + 1]);  // expand child A first
             const BVHEntry& A = blas[a];
             const BVHEntry& B = blas[a + 1];
-            const size_t r = 4 * size_t(dref[g]);
-            rec[r] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z, bits(ra));
-            rec[r + 1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z, bits(rb));
-            rec[r + 2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
-            rec[r + 3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
+            put_pair(&rec[4 * size_t(dref[g])], A, B, ra, rb);
         }
         std::memcpy(dm[mi].w2l, m.worldToLocal.m, sizeof dm[mi].w2l);
         dm[mi].root_ref = root;

@@ -259,12 +259,11 @@ __global__ __launch_bounds__(256, HG_TRACE_WAVES) void hg_wf_trace(const HgKerne
         // ---- inner nodes (while-while: all lanes descend together until each holds a leaf) ----
         while (__any(st == ST_TRAV && !(node & HG_LEAF_BIT))) {
             if (st == ST_TRAV && !(node & HG_LEAF_BIT)) {
-                const float4* rec = kp.nodes + 4 * node;
-                const float4 a_lo = rec[0], a_hi = rec[1], b_lo = rec[2], b_hi = rec[3];
-                const float dA = ray_aabb(xyz(a_lo), xyz(a_hi), lo, inv);
-                const float dB = ray_aabb(xyz(b_lo), xyz(b_hi), lo, inv);
+                const NodePair np = node_pair(kp, node);
+                float dA, dB;
+                pair_dist(np, lo, inv, dA, dB);
                 c_aabb += 2;
-                const uint32_t refA = __float_as_uint(a_lo.w), refB = __float_as_uint(a_hi.w);
+                const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
                 // reference: push far, push near, pop near (:430-444) == keep near in the register
                 const bool bFirst = dB < dA;
                 const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
