@@ -84,9 +84,10 @@ def test_gpu_coalesced_frames_flush_at_every_observation(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg_name", ["C3", "C5"])
+@pytest.mark.parametrize("cfg_name", ["C3", "C5", "C2"])
 def test_gpu_one_frame_launches_match_batched_full_size(gpu, cfg_name):
-    """BASELINE's C3 (871k dragon, streaming kernel) and C5 (glass + cubemap, regenerating kernel) at 1920x1080:
+    """BASELINE's C3 (871k dragon, streaming kernel), C5 (glass + cubemap, regenerating kernel) and C2 (Cornell box,
+    streaming kernel on a shallow BVH) at 1920x1080:
     64 x hg_render(1) from a cleared accumulator is bit-identical to one hg_render(64) over the whole image, and a
     band of rows of it equals the live oracle."""
     packed, params, cube = _full(cfg_name)
