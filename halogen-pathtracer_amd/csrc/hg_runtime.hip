@@ -1020,9 +1020,10 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 if (e == hipSuccess)
                     e = stream_k ? hg_launch_mega_stream(kc, mblock, c->counters_on != 0, L.stream)
                                  : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, L.stream);
-                if (e == hipSuccess && c->timing) {
-                    e = hipEventRecord(tev.second, L.stream);
-                    c->pending_trace.push_back(tev);
+                if (c->timing && tev.first) {  // a pair goes to drain_events only with both ends recorded
+                    if (e == hipSuccess) e = hipEventRecord(tev.second, L.stream);
+                    if (e == hipSuccess) c->pending_trace.push_back(tev);
+                    else c->free_events.push_back(tev);
                 }
                 if (e == hipSuccess) e = hipEventRecord(L.traced, L.stream);
                 if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, L.traced, 0);
