@@ -258,9 +258,18 @@ __device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f,
 // (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md;
 // the non-temporal hint on these loads: C3 -9.7 %, C3F -10 %, tools/sweeps/sweep_r03_o.jsonl.)
 __device__ __forceinline__ void tri_load(const HgKernelParams& kp, uint32_t ti, float4& a, float4& b, float& cz) {
+#if HG_TRI_AOS
+    typedef float hg_v4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned 16-B loads
+    const char* p = reinterpret_cast<const char*>(kp.tri_a) + ti * 36u;
+    const hg_v4u va = *reinterpret_cast<const hg_v4u*>(p), vb = *reinterpret_cast<const hg_v4u*>(p + 16);
+    a = make_float4(va.x, va.y, va.z, va.w);
+    b = make_float4(vb.x, vb.y, vb.z, vb.w);
+    cz = *reinterpret_cast<const float*>(p + 32);
+#else
     a = ld_off(kp.tri_a, ti << 4);
     b = ld_off(kp.tri_b, ti << 4);
     cz = ld_off(kp.tri_c, ti << 2);
+#endif
 }
 
 // Load of scene data the kernel never writes (mesh records, spheres) through the constant address space: a

@@ -110,6 +110,9 @@
 #ifndef HG_NODE_PREFETCH
 #define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
 #endif
+#ifndef HG_TRI_AOS
+#define HG_TRI_AOS 1  // triangles as packed 36-B records (v0, e1, e2; tri_load's three loads on one record) instead of
+#endif            // the three streams tri_a / tri_b / tri_c (a leaf's triangles on fewer cache lines)
 #ifndef HG_PAIR_SOA
 #define HG_PAIR_SOA 0  // child-pair records coordinate by coordinate, A and B side by side: packed-FP32 box tests
 #endif             // (node_pair / pair_dist in hg_device.h; the record writer in hg_runtime.hip)

@@ -685,9 +685,18 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if ((rc = upload(c, c->meshes, dm.data(), dm.size() * sizeof(HgDevMesh)))) return rc;
     if ((rc = upload(c, c->nodes, rec.data(), rec.size() * sizeof(float4)))) return rc;
     if ((rc = upload(c, c->leaves, leaf.data(), leaf.size() * sizeof(uint2)))) return rc;
+#if HG_TRI_AOS
+    std::vector<float> t9(ta.size() * 9);  // (a, b, c) of tri_load, packed per triangle
+    for (size_t i = 0; i < ta.size(); ++i) {
+        const float v[9] = {ta[i].x, ta[i].y, ta[i].z, ta[i].w, tb[i].x, tb[i].y, tb[i].z, tb[i].w, tc[i]};
+        std::memcpy(&t9[9 * i], v, sizeof v);
+    }
+    if ((rc = upload(c, c->tri_a, t9.data(), t9.size() * sizeof(float)))) return rc;
+#else
     if ((rc = upload(c, c->tri_a, ta.data(), ta.size() * sizeof(float4)))) return rc;
     if ((rc = upload(c, c->tri_b, tb.data(), tb.size() * sizeof(float4)))) return rc;
     if ((rc = upload(c, c->tri_c, tc.data(), tc.size() * sizeof(float)))) return rc;
+#endif
     if ((rc = upload(c, c->normals, nrm.data(), nrm.size() * sizeof(float4)))) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));  // host staging vectors die at return
     c->n_spheres = n_spheres;
