@@ -66,8 +66,10 @@ struct hg_ctx {
         bool tile_order_valid = false;
         int64_t frames_since_order = 0;  // frames traced on this stream since its last sort
     };
+    static_assert(HG_TRACE_LANES_BIG >= 1 && HG_TRACE_LANES_BIG <= HG_TRACE_LANES, "HG_TRACE_LANES_BIG out of range");
     TraceLane lanes[HG_TRACE_LANES];
-    int next_lane = 0;
+    int next_lane = 0;     // chunks of at most HG_QUEUE_MAX_FRAMES frames: every lane in turn
+    int next_lane_big = 0;  // longer chunks: lanes [0, HG_TRACE_LANES_BIG) in turn
     uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
     size_t poll_cap = 0;
     std::vector<hipEvent_t> poll_events;

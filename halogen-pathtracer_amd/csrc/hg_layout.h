@@ -173,7 +173,20 @@
 #define HG_COALESCE 32  // default HG_OPT_COALESCE: frames of consecutive hg_render calls held for one launch
 #endif
 #ifndef HG_TRACE_LANES
-#define HG_TRACE_LANES 2  // trace streams of the render pipeline (hg_ctx.h): chunks traced in turn on them, blended in order
+#define HG_TRACE_LANES 4  // trace streams of the render pipeline (hg_ctx.h): chunks traced in turn on them, blended in
+#endif                    // order.  1-frame launches, C3: 2 streams 1,970, 3: 2,143, 4: 2,265, 6: 2,242, 8: 2,302 Mpaths/s
+                          // (tools/sweeps/sweep_r03_u/v.txt; streams 3+ on their own hardware queues, HG_LANE_STREAMS)
+#ifndef HG_TRACE_LANES_BIG
+#define HG_TRACE_LANES_BIG 2  // of those, the ones chunks of more than HG_QUEUE_MAX_FRAMES frames take in turn (a third
+#endif                        // 64-frame launch beside two others: C3 -1.5 %)
+#ifndef HG_LANE_STREAMS
+// How the trace streams are created.  HIP spreads plain streams over a pool of GPU_MAX_HW_QUEUES (default 4) hardware
+// queues shared by every stream of the process, and two streams on one queue run their launches one after the other:
+// a third plain trace stream cost 1-frame launches 16 % (1,663 vs 1,970; 2,111 with GPU_MAX_HW_QUEUES=8).  A stream
+// created with a CU mask gets a hardware queue of its own.  0: plain, 1: all with an all-CU mask, 2: all with the
+// greatest stream priority (also a queue of its own: 2,121 at 3 streams), 3: plain for the first HG_TRACE_LANES_BIG
+// (non-blocking, as before), an all-CU mask for the others (4 streams: 2,266 vs 2,260 all masked; batched equal).
+#define HG_LANE_STREAMS 3
 #endif
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
