@@ -453,7 +453,11 @@ hipError_t create_lane_stream(const hg_ctx* c, int lane, hipStream_t* s) {
     if (HG_LANE_STREAMS == 3 && lane < HG_TRACE_LANES_BIG) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     std::vector<uint32_t> mask(size_t((c->n_cu + 31) / 32), 0u);
     for (int i = 0; i < c->n_cu; ++i) mask[size_t(i) / 32] |= 1u << (i % 32);
-    return hipExtStreamCreateWithCUMask(s, uint32_t(mask.size()), mask.data());
+    // (CU-masked streams are blocking with respect to the legacy null stream, unlike the plain ones.)  Where the
+    // runtime refuses CU masks, a plain stream: the same results, only the queue sharing above comes back.
+    if (hipExtStreamCreateWithCUMask(s, uint32_t(mask.size()), mask.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 #elif HG_LANE_STREAMS == 2
     (void)lane;
     int lo = 0, hi = 0;
