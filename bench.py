@@ -307,6 +307,9 @@ def main():
                     help="profiling aid: only the per-frame leg's timed part (no headline line)")
     ap.add_argument("--launch-frames", type=int, default=1, help="--per-frame-only: frames per hg_render call")
     ap.add_argument("--coalesce", type=int, default=1, help="--per-frame-only: HG_OPT_COALESCE (1: every call launches)")
+    ap.add_argument("--display", choices=["none", "sync", "pipelined"], default="none",
+                    help="--per-frame-only: the display readback (hg_readback_begin/_end) after every call, as the "
+                         "per_frame leg's with_display_readback")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
@@ -413,8 +416,18 @@ def main():
         ctx.reset_counters()
         ctx.synchronize()
         t0 = time.perf_counter()
+        pending = 0
         for _ in range(args.steps * frames_per_step // args.launch_frames):
             ctx.render(args.launch_frames, True)
+            if args.display != "none":
+                ctx.readback_begin()
+                pending += 1
+                if args.display == "sync" or pending == 2:
+                    ctx.readback_end(W, H, copy=False)
+                    pending -= 1
+        while pending:
+            ctx.readback_end(W, H, copy=False)
+            pending -= 1
         ctx.synchronize()
         dt = time.perf_counter() - t0
         c = ctx.counters()
