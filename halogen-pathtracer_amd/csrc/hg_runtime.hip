@@ -1012,7 +1012,7 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 }
             }
             HgKernelParams kc = kp;
-            kc.resident_waves = uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES;
+            const uint32_t slots = uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES;
             for (int done = 0; done < n_frames && e == hipSuccess;) {  // chunks at frame boundaries change nothing
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 // short chunks (the reference's one dispatch per frame) in turn on every trace stream, so that more
@@ -1033,6 +1033,18 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 kc.spill = spill_bytes ? static_cast<uint32_t*>(L.spill.p) : nullptr;
                 // the persistent work-queue form for launches of few frames (the reference's one dispatch per frame)
                 kc.queue = stream_k && kc.n_frames <= HG_QUEUE_MAX_FRAMES ? static_cast<uint32_t*>(L.queue.p) : nullptr;
+                // Persistent waves of a queue launch.  A launch's end costs each of its waves the time its last paths
+                // take, with its lanes draining; fewer, longer-lived waves pay that less often.  So while two or more
+                // other traces are in flight (which fill the slots), a launch takes slots / min(HG_QUEUE_WAVES_DIV,
+                // traces in flight + 1); alone or beside one other (e.g. a caller that reads every frame back), all.
+                kc.resident_waves = slots;
+                if (kc.queue && HG_QUEUE_WAVES_DIV > 1) {
+                    int busy = 0;
+                    for (const hg_ctx::TraceLane& O : c->lanes)
+                        if (&O != &L && O.blend_pending && hipEventQuery(O.traced) == hipErrorNotReady) ++busy;
+                    (void)hipGetLastError();  // hipErrorNotReady is a status here, not an error for the launch check
+                    if (busy >= 2) kc.resident_waves = slots / uint32_t(std::min(HG_QUEUE_WAVES_DIV, busy + 1));
+                }
                 kc.tile_order = nullptr;
                 kc.tile_cost = ordered ? static_cast<unsigned long long*>(L.tile_cost.p) : nullptr;
                 // this stream's buffers are free once the blend of its previous chunk has read them
