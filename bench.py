@@ -249,6 +249,11 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and ok else None,
             "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS if traffic and ok else None,
             "hbm_peak_gbs": HBM_PEAK_GBS,
+            "hbm_target_note": "north_star's >= 50 % of the HBM roofline during traversal does not apply: the scene "
+                               "is cache-resident (L1/L2/Infinity Cache serve the BVH), so traffic_frac is the DRAM-side "
+                               "share, not a bound; the traversal is bound by the vector-memory data path "
+                               "(vmem_unit_busy.td_busy) and frac prices the VALU issue rate that follows from it "
+                               "(DESIGN.md sections 4.5, 10)",
             "write_bytes_per_launch": pmc.get("write_bytes_per_launch"),
             "logical_bytes_per_launch": logical_per_launch,
             "logical_gbs": logical_per_launch / mean_launch_s / 1e9 if logical_per_launch and ok else None,
