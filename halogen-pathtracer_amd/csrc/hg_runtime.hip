@@ -997,8 +997,14 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         const size_t tb = size_t(tiles) * sizeof(uint32_t);
         if (pipelined) {
             // the trace streams' buffers, grown only while idle (the lanes beyond HG_TRACE_LANES_BIG trace short chunks only)
+            // the streams beyond HG_TRACE_LANES_BIG only when this launch has a chunk of at most HG_QUEUE_MAX_FRAMES
+            // frames (the first, the last, or all of them), the rotation below that takes them
+            const int last_chunk = n_frames % chunk_max;
+            const bool short_chunks = std::min(n_frames, chunk_max) <= HG_QUEUE_MAX_FRAMES ||
+                                      (last_chunk != 0 && last_chunk <= HG_QUEUE_MAX_FRAMES);
             for (int li = 0; li < HG_TRACE_LANES; ++li) {
                 hg_ctx::TraceLane& L = c->lanes[li];
+                if (li >= HG_TRACE_LANES_BIG && !short_chunks) continue;
                 const int fmax = std::min(n_frames, li < HG_TRACE_LANES_BIG ? chunk_max
                                                                              : std::min(chunk_max, HG_QUEUE_MAX_FRAMES));
                 int rc = ensure_quiet(c, L.frame_color, per_frame * size_t(fmax));
