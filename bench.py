@@ -413,9 +413,10 @@ def main():
     setup_s = time.perf_counter() - t_setup
 
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
-    if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step, then steps x frames x hg_render(1)
+    if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step of the same launches, then steps x frames x hg_render(1)
         ctx.set_option(abi.HG_OPT_COALESCE, args.coalesce)
-        ctx.render(frames_per_step, True)
+        for _ in range(frames_per_step // args.launch_frames):  # warm-up step of the timed launches (their buffers)
+            ctx.render(args.launch_frames, True)
         ctx.clear_accumulation()
         ctx.set_params(params)
         ctx.reset_counters()
