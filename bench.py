@@ -23,7 +23,8 @@ DRAM-side bytes ("traffic") against 8 TB/s and SURVEY.md §8d's logical bytes (3
 triangle test, 64 B per mesh transform, 44 B per sphere test, 284 B per accepted hit, 48 B per pixel-frame)
 are reported beside it.
 cpu_baseline: the CPU oracle (oracle/hg_oracle.c, a scalar C restatement of the same kernel) on rank 0 at N=1,
-on a stratified sample of row bands of the same workload, threads = min(16, cpus).
+on a stratified sample of row bands of the same workload, threads = min(16, CPUs in this process's affinity mask); the
+line reports the affinity CPUs and the physical cores among them beside the thread count.
 """
 from __future__ import annotations
 
@@ -268,12 +269,29 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "counters_library_matches": (pmc.get("library_sha256") == lib_sha) if pmc.get("library_sha256") else None}
 
 
+def host_cpus() -> dict:
+    """The CPUs this process may run on (sched_getaffinity), the physical cores among them (distinct (package, core)
+    pairs from sysfs topology), and the machine's logical CPU count (os.cpu_count: on the GPU box the whole machine,
+    many times this process's share)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores = set()
+    for cpu in aff:
+        t = Path(f"/sys/devices/system/cpu/cpu{cpu}/topology")
+        try:
+            cores.add((t.joinpath("physical_package_id").read_text().strip(), t.joinpath("core_id").read_text().strip()))
+        except OSError:
+            cores.add(("?", str(cpu)))
+    return {"affinity_cpus": len(aff), "physical_cores_in_affinity": len(cores), "machine_logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(packed, params, cube, width, height, seconds, threads):
-    """Oracle on stratified 2-row bands of frame 1 until `seconds` of wall time are used."""
+    """Oracle on stratified 2-row bands of frame 1 until `seconds` of wall time are used.  The plain oracle build: its
+    traversal holds no diagnostics (those live in the stats build, oracle/Makefile)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import hg_oracle  # test-infra import, cpu_baseline leg only
 
     hg_oracle.lib()
+    assert hg_oracle.lib().hgo_stats_build() == 0
     n_bands = 27
     order = [int(b) for b in np.linspace(0, height - 2, n_bands).astype(int)]
     paths = 0
@@ -291,9 +309,13 @@ def cpu_baseline(packed, params, cube, width, height, seconds, threads):
             break
     params.frameCount = 1
     dt = time.perf_counter() - t0
-    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+    host = host_cpus()
+    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "threads": threads, **host,
+            "kind": "port",
             "sample": f"{n_bands} stratified 2-row bands x {width} px (every ~{height // n_bands} rows) x {frames} "
-                      f"frames = {paths} paths in {dt:.1f} s; scalar C oracle (oracle/hg_oracle.c), {threads} threads"}
+                      f"frames = {paths} paths in {dt:.1f} s; scalar C oracle (oracle/hg_oracle.c, plain build), "
+                      f"{threads} threads on {host['affinity_cpus']} allowed CPUs "
+                      f"({host['physical_cores_in_affinity']} physical cores)"}
 
 
 def main():
@@ -614,7 +636,9 @@ def main():
         if world == 1 and not emu and args.config == "C3" and not args.no_counters and not args.no_framed:
             result["framed"] = framed_measurement(ctx, packed, s, W, H, frames_per_step, max(2, args.steps // 4))
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
+            # the box's CPU share is 16 (OMP_NUM_THREADS there); never more threads than CPUs this process may use
+            threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                                 else (os.cpu_count() or 1)))
             result["cpu_baseline"] = cpu_baseline(packed, params, cube, W, H, args.cpu_seconds, threads)
         print(json.dumps(result), flush=True)
     if comm is not None:

@@ -22,6 +22,10 @@
 
 #include "hg_fmath.h"
 
+#ifndef HGO_STATS
+#define HGO_STATS 0 /* 1: the stats build (diagnostic counts, see hgo_stack_stats) */
+#endif
+
 /* ------------------------------------------------------------------------------------------------
  * small vector helpers, literal HLSL semantics (no FMA contraction; compiled -ffp-contract=off)
  * ---------------------------------------------------------------------------------------------- */
@@ -156,6 +160,10 @@ typedef struct {
     int msp;               /* mediumStackPointer */
     int tri_tests, aabb_tests; /* TriangleTests / AABBTests statics */
     hg_counters cnt;
+#if HGO_STATS /* diagnostics of the stats build (merge_stats) */
+    uint64_t st_overflow, st_visit[6];
+    int32_t st_max;
+#endif
 } tstate;
 
 #define ID_FOCAL 0u
@@ -429,36 +437,52 @@ static void scene_isect_spheres(tstate* t, const ray_t* ray, hit_t* closest) {
 #define NODE_STACK 64 /* reference: int NodeStack[32] (:397); 33 can be needed at depth cap 32, see DESIGN.md */
 #define REF_NODE_STACK 32 /* the reference's array size: a push at index >= 32 is out of bounds in HC:397-444 */
 
-/* Diagnostics (test infra): mesh traversals whose stack would outgrow the reference's NodeStack[32], and the
- * deepest stack seen, since the last hgo_stack_stats(reset=1). */
-static _Atomic uint64_t g_stack_overflow_traversals;
-static _Atomic int32_t g_stack_max;
+/* Diagnostics (test infra; tools/stack_depth.py, tools/visit_stats.py, tests/test_oracle.py): compiled only into the
+ * stats build (HGO_STATS=1, build/libhgoracle_stats.so).  The plain build, which the parity tests and bench.py's
+ * cpu_baseline load, has none of it in the traversal.  The stats build counts per thread (tstate) and merges once per
+ * render job, so even there no shared cache line sits in the traversal loop.
+ *   stack: mesh traversals whose stack would outgrow the reference's NodeStack[32], and the deepest stack seen;
+ *   visits: inner-node visits by how many of the two children the exact test keeps (t < closest), for mesh roots and
+ *           for deeper nodes: [root 0/1/2, inner 0/1/2].
+ * All since the last reset (hgo_stack_stats / hgo_visit_stats with reset=1). */
+static pthread_mutex_t g_stats_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t g_stack_overflow_traversals;
+static int32_t g_stack_max;
+static uint64_t g_visit_ok[6];
+int hgo_stats_build(void) { return HGO_STATS; }
 void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t reset) {
+    pthread_mutex_lock(&g_stats_mu);
     if (overflow_traversals) *overflow_traversals = g_stack_overflow_traversals;
-    if (max_depth) *max_depth = g_stack_max;
+    if (max_depth) *max_depth = HGO_STATS ? g_stack_max : -1;
     if (reset) {
         g_stack_overflow_traversals = 0;
         g_stack_max = 0;
     }
+    pthread_mutex_unlock(&g_stats_mu);
 }
-/* the popped node was the mesh's root: the stack was empty after its pop and nothing had been pushed before */
-static int stack_is_root(int sp, int high) { return sp == 0 && high == 1; }
-static void note_stack(int high) {
-    if (high > REF_NODE_STACK) g_stack_overflow_traversals++;
-    int32_t cur = g_stack_max;
-    while (high > cur && !__atomic_compare_exchange_n((int32_t*)&g_stack_max, &cur, high, 0, __ATOMIC_RELAXED,
-                                                       __ATOMIC_RELAXED)) {
-    }
-}
-
-/* Diagnostics (test infra, tools/visit_stats.py): inner-node visits by how many of the two children the exact test
- * keeps (t < closest), for mesh roots and for deeper nodes: [root 0/1/2, inner 0/1/2]. */
-static _Atomic uint64_t g_visit_ok[6];
 void hgo_visit_stats(uint64_t out[6], int32_t reset) {
+    pthread_mutex_lock(&g_stats_mu);
     for (int k = 0; k < 6; ++k) {
         if (out) out[k] = g_visit_ok[k];
         if (reset) g_visit_ok[k] = 0;
     }
+    pthread_mutex_unlock(&g_stats_mu);
+}
+#if HGO_STATS
+/* the popped node was the mesh's root: the stack was empty after its pop and nothing had been pushed before */
+static int stack_is_root(int sp, int high) { return sp == 0 && high == 1; }
+#endif
+/* a thread's counts into the globals (once per render job / traced pixel) */
+static void merge_stats(const tstate* t) {
+#if HGO_STATS
+    pthread_mutex_lock(&g_stats_mu);
+    g_stack_overflow_traversals += t->st_overflow;
+    if (t->st_max > g_stack_max) g_stack_max = t->st_max;
+    for (int k = 0; k < 6; ++k) g_visit_ok[k] += t->st_visit[k];
+    pthread_mutex_unlock(&g_stats_mu);
+#else
+    (void)t;
+#endif
 }
 
 /* get_ray_scene_intersection_mesh, :378-472 */
@@ -478,10 +502,15 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
         ray_t pre = local;
         pre.d = v3(1.0f / local.d.x, 1.0f / local.d.y, 1.0f / local.d.z);
         uint32_t stack[NODE_STACK];
-        int sp = 0, high = 1;
+        int sp = 0;
+#if HGO_STATS
+        int high = 1;
+#endif
         stack[sp++] = md->accelerationBufferOffset;
         while (sp > 0) {
+#if HGO_STATS
             if (sp > high) high = sp;
+#endif
             const BVHEntry* node = &sc->blas[stack[--sp]];
             if (node->triangleCount > 0) {
                 for (uint32_t k = 0; k < node->triangleCount; k++) {
@@ -502,7 +531,9 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
                 float dB = ray_aabb(fromv(B->boundingCornerA), fromv(B->boundingCornerB), &pre);
                 t->aabb_tests += 2;
                 t->cnt.aabb_tests += 2;
-                g_visit_ok[(stack_is_root(sp, high) ? 0 : 3) + (dA < closest.rayT) + (dB < closest.rayT)]++;
+#if HGO_STATS
+                t->st_visit[(stack_is_root(sp, high) ? 0 : 3) + (dA < closest.rayT) + (dB < closest.rayT)]++;
+#endif
                 /* pushes beyond NODE_STACK are dropped; hg_upload_scene rejects trees deep enough to
                  * reach that, so this is a guard, not behaviour */
                 if (dB < dA) {
@@ -514,7 +545,10 @@ static void scene_isect_meshes(tstate* t, const ray_t* ray, hit_t* closestHit) {
                 }
             }
         }
-        note_stack(high);
+#if HGO_STATS
+        if (high > REF_NODE_STACK) t->st_overflow++;
+        if (high > t->st_max) t->st_max = high;
+#endif
     }
     if (closest.rayT < (closestHit->rayT - eps) && closest.rayT < t->p->viewParameters.w) {
         const HalogenMeshData* md = &sc->meshes[closest.mesh];
@@ -851,6 +885,7 @@ void hgo_trace_pixel(const hgo_scene* scene, const hg_params* params, uint32_t x
     t.p = params;
     t.frame = (uint32_t)frame;
     f3 c = halogen_compute_pixel(&t, x, y);
+    merge_stats(&t);
     rgb[0] = c.x;
     rgb[1] = c.y;
     rgb[2] = c.z;
@@ -906,6 +941,7 @@ static void* render_job(void* arg) {
         }
     }
     j->cnt = t.cnt;
+    merge_stats(&t);
     return NULL;
 }
 

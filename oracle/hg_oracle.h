@@ -62,8 +62,11 @@ int hgo_render(const hgo_scene* scene, const hg_params* params, int32_t n_frames
 void hgo_trace_pixel(const hgo_scene* scene, const hg_params* params, uint32_t x, uint32_t y, int32_t frame,
                      float rgb[3], hg_counters* counters);
 
-/* Diagnostics: mesh traversals (since the last reset) whose node stack would hold more than the reference's
- * NodeStack[32] entries (HC:397), and the deepest stack seen. */
+/* Diagnostics, collected only by the stats build (HGO_STATS=1: build/libhgoracle_stats.so; the plain build keeps
+ * the traversal free of them and reports zeros, max_depth -1).  hgo_stats_build() says which build this is.
+ * Mesh traversals (since the last reset) whose node stack would hold more than the reference's NodeStack[32]
+ * entries (HC:397), and the deepest stack seen. */
+int hgo_stats_build(void);
 void hgo_stack_stats(uint64_t* overflow_traversals, int32_t* max_depth, int32_t reset);
 /* Diagnostics: inner-node visits by the number of children the exact test keeps: [root 0/1/2, inner 0/1/2]. */
 void hgo_visit_stats(uint64_t out[6], int32_t reset);

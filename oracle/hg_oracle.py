@@ -15,6 +15,9 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "build" / "libhgoracle.so"
+# the stats build (HGO_STATS=1): the same oracle with the traversal diagnostics compiled in (stack_stats, visit_stats);
+# the plain build above has none of them in its traversal loop (it is the parity checker and the CPU baseline)
+LIB_STATS = HERE / "build" / "libhgoracle_stats.so"
 
 
 class HgoScene(C.Structure):
@@ -24,7 +27,7 @@ class HgoScene(C.Structure):
                 ("cube_texels", C.c_void_p), ("cube_face_size", C.c_int32), ("cube_mips", C.c_int32)]
 
 
-_lib = None
+_libs: dict = {}
 
 
 def build() -> Path:
@@ -32,12 +35,13 @@ def build() -> Path:
     return LIB
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+def lib(stats: bool = False):
+    """The plain oracle, or (stats=True) its stats build."""
+    path = LIB_STATS if stats else LIB
+    if path not in _libs:
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         u32 = C.c_uint32
         L.hgo_pcg_hash.restype = u32
         L.hgo_pcg_hash.argtypes = [u32]
@@ -79,8 +83,10 @@ def lib():
         L.hgo_cube_sample.argtypes = [C.POINTER(HgoScene), fp, C.c_int32, fp]
         L.hgo_cube_adjacent.restype = None
         L.hgo_cube_adjacent.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]
-        _lib = L
-    return _lib
+        L.hgo_stats_build.restype = C.c_int
+        L.hgo_stats_build.argtypes = []
+        _libs[path] = L
+    return _libs[path]
 
 
 def make_scene(packed, cubemap=None) -> tuple[HgoScene, list]:
@@ -115,8 +121,9 @@ class Counters(C.Structure):  # hg_counters layout (include/halogen_abi.h), comp
 
 
 def render(packed, params, n_frames: int, accumulate: bool = True, acc: np.ndarray | None = None,
-           cubemap=None, pix_range=None, threads: int | None = None):
-    """Render n_frames into acc ((H, W, 4) float32, row-major); returns (acc, counters dict)."""
+           cubemap=None, pix_range=None, threads: int | None = None, stats: bool = False):
+    """Render n_frames into acc ((H, W, 4) float32, row-major); returns (acc, counters dict).  stats=True renders
+    through the stats build, which also feeds stack_stats() / visit_stats()."""
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)
     if acc is None:
         acc = np.zeros((H, W, 4), dtype=np.float32)
@@ -124,7 +131,7 @@ def render(packed, params, n_frames: int, accumulate: bool = True, acc: np.ndarr
     cnt = Counters()
     p0, p1 = pix_range if pix_range is not None else (0, W * H)
     threads = threads or min(os.cpu_count() or 1, 64)
-    rc = lib().hgo_render(C.byref(scene), C.byref(params), n_frames, 1 if accumulate else 0, acc.ctypes.data, p0, p1,
+    rc = lib(stats).hgo_render(C.byref(scene), C.byref(params), n_frames, 1 if accumulate else 0, acc.ctypes.data, p0, p1,
                           threads, C.byref(cnt))
     if rc != 0:
         raise RuntimeError(f"hgo_render failed: {rc}")
@@ -133,16 +140,18 @@ def render(packed, params, n_frames: int, accumulate: bool = True, acc: np.ndarr
 
 
 def stack_stats(reset: bool = False) -> tuple[int, int]:
-    """(mesh traversals whose node stack outgrew the reference's NodeStack[32], deepest stack) since the last reset."""
+    """(mesh traversals whose node stack outgrew the reference's NodeStack[32], deepest stack) since the last reset, over
+    the renders made with stats=True."""
     n, d = C.c_uint64(0), C.c_int32(0)
-    lib().hgo_stack_stats(C.byref(n), C.byref(d), 1 if reset else 0)
+    lib(True).hgo_stack_stats(C.byref(n), C.byref(d), 1 if reset else 0)
     return int(n.value), int(d.value)
 
 
 def visit_stats(reset: bool = False) -> dict:
-    """Inner-node visits by the number of children the exact test keeps (0/1/2), for mesh roots and deeper nodes."""
+    """Inner-node visits by the number of children the exact test keeps (0/1/2), for mesh roots and deeper nodes, over
+    the renders made with stats=True."""
     out = (C.c_uint64 * 6)()
-    lib().hgo_visit_stats(out, 1 if reset else 0)
+    lib(True).hgo_visit_stats(out, 1 if reset else 0)
     return {"root": [int(x) for x in out[:3]], "inner": [int(x) for x in out[3:]]}
 
 

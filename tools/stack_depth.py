@@ -33,7 +33,7 @@ W, H = cfg.width, cfg.height
 y0, y1 = (int(v) for v in args.rows.split(":")) if args.rows else (0, H)
 hg_oracle.stack_stats(reset=True)
 t0 = time.time()
-_, cnt = hg_oracle.render(packed, params, args.frames, True, cubemap=cube, pix_range=(y0 * W, y1 * W))
+_, cnt = hg_oracle.render(packed, params, args.frames, True, cubemap=cube, pix_range=(y0 * W, y1 * W), stats=True)
 over, deepest = hg_oracle.stack_stats()
 print(json.dumps({"config": args.config, "width": W, "rows": [y0, y1], "frames": args.frames,
                   "paths": cnt["paths"], "rays": cnt["rays"], "mesh_traversals": cnt["mesh_visits"],

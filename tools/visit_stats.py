@@ -25,7 +25,7 @@ W, H = cfg.width, cfg.height
 hg_oracle.visit_stats(reset=True)
 tot = {"paths": 0, "aabb_tests": 0}
 for y in np.linspace(0, H - 2, 9).astype(int):
-    _, cnt = hg_oracle.render(packed, params, 2, True, cubemap=cube, pix_range=(int(y) * W, (int(y) + 2) * W), threads=8)
+    _, cnt = hg_oracle.render(packed, params, 2, True, cubemap=cube, pix_range=(int(y) * W, (int(y) + 2) * W), threads=8, stats=True)
     tot["paths"] += cnt["paths"]
     tot["aabb_tests"] += cnt["aabb_tests"]
 v = hg_oracle.visit_stats()
