@@ -62,6 +62,7 @@ public static class HalogenNative
         public ulong primary_misses;
         public ulong exec_fallbacks;
         public double trace_busy_ms;
+        public ulong order_faults;
     }
 
     public const int HG_OK = 0;
@@ -69,7 +70,7 @@ public static class HalogenNative
                      HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9;
-    public const int HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2, HG_BUILD_CHECK_EXEC = 1;
+    public const int HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2, HG_BUILD_CHECK_EXEC = 1, HG_BUILD_NO_REGEN_ITEMS = 2;
     public const int HG_COMM_ID_BYTES = 128, HG_COMM_RCCL = 1, HG_COMM_PEER = 2;
 
     [DllImport(Lib)] public static extern int hg_abi_version();

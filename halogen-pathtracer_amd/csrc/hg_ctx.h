@@ -61,7 +61,9 @@ struct hg_ctx {
         // was still adding to: the counting sort's two passes then disagreed and wrote out of range.)
         DevBuf tile_cost;              // per local tile, wave-clock cost since this stream's last sort
         DevBuf tile_order;             // the cost order this stream's launches read
-        DevBuf queue;                  // kQueue launches: the 8 unit heads (zeroed per launch)
+        DevBuf order_scratch;          // hg_order_tiles: histogram and claims (zeroed at allocation, left zeroed)
+        DevBuf queue;                  // kQueue launches: the 8 unit heads + exit count (zeroed at allocation; the
+                                       // last wave of each launch zeroes them again)
         bool tile_cost_valid = false;  // tile_cost holds costs for this tiling
         bool tile_order_valid = false;
         int64_t frames_since_order = 0;  // frames traced on this stream since its last sort

@@ -92,9 +92,6 @@
 #ifndef HG_LEAF_DIST
 #define HG_LEAF_DIST 1  // streaming traversal: a round's (ray, triangle) pairs dealt over all 64 lanes, LDS min-reduce
 #endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweeps/sweep52.txt)
-#ifndef HG_ORDER_BUCKETS
-#define HG_ORDER_BUCKETS 1024  // hg_order_tiles: cost buckets of the longest-first order (tile-index order within one)
-#endif
 #ifndef HG_PINHOLE_FAST
 #define HG_PINHOLE_FAST 1  // camera_ray skips the focal-disc sample when the disc radius is 0 (same bits, hg_device.h)
 #endif
@@ -196,6 +193,10 @@
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif
+// The queue of a kQueue launch: 8 unit heads, 128 B apart (words 32 h), then the count of waves that have left (its own
+// 128-B line): the last wave out zeroes them for the next launch (the runtime zeroes the buffer once, at allocation)
+#define HG_QUEUE_DONE_WORD 256u
+#define HG_QUEUE_BYTES (9u * 128u)
 #ifndef HG_ITEMS_PIXEL_MAJOR
 #define HG_ITEMS_PIXEL_MAJOR 1  // items k -> (pixel k / frames, frame k % frames): a wave's lanes trace one pixel's frames
                                 // (with HG_FC_SLOT_MAJOR: C3 +0.4 %, C2 +0.5 %, C5 -0.4 %; tools/sweeps/sweep_r02_be/bf)

@@ -229,84 +229,144 @@ struct TileItems {
     }
 };
 
-// One workgroup of 1024 threads: tile_order = the local tiles by descending cost, STABLE (the costs must not change
-// during the sort: the runtime sorts a trace stream's own costs on that stream, hg_ctx.h TraceLane) (equal buckets keep
-// tile-index order, so the dispatch order of a launch is a deterministic function of the recorded costs), then the
-// costs are cleared for the next launch.  Counting sort over 1024 linear cost buckets (bucket 0 = most expensive):
-//   1. per-bucket counts over all tiles, exclusive prefix = each bucket's start;
-//   2. tiles in chunks of 1024 in index order: a tile's place = its bucket's running start + the number of earlier
-//      tiles of the same bucket in the chunk (inside a wave: a 10-ballot bucket match; across the chunk's 16 waves:
-//      per-wave bucket counts in LDS), then the running starts advance by the chunk's counts.
-// Costs all 0 (nothing recorded): every tile falls in one bucket and the order is the identity.
-__global__ __launch_bounds__(1024) void hg_order_tiles(unsigned long long* __restrict__ cost,
-                                                       uint32_t* __restrict__ order, uint32_t n) {
-    __shared__ uint32_t start[1024];        // running start of each bucket
-    __shared__ uint16_t wcount[16][1024];   // chunk: tiles of bucket b in wave w (then: exclusive prefix over w)
-    __shared__ unsigned long long cmax;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    if (t == 0) cmax = 0;
-    start[t] = 0;
+// Cost order (hg_render, per trace stream): tile_order = the local tiles, most expensive first, then the costs are
+// cleared for the next launches.  A counting sort over 1024 log-scale cost buckets (16 per octave of the wave-clock
+// cost: bucket 0 the most expensive; two tiles share one only within ~4 % of each other), in two launches of one-wave
+// workgroups (1,024 tiles each) with 8-12 KB of LDS and few registers, so that they fit on CUs beside the persistent
+// trace waves of the other streams (round 3's single 1,024-thread, 36-KB workgroup waited for a whole CU to drain:
+// ~1 ms per sort at the one-dispatch-per-frame operating point):
+//   hg_order_hist     each workgroup histograms its tiles in LDS and adds the counts to the global histogram;
+//   hg_order_scatter  each workgroup derives the buckets' starts (exclusive prefix of the global histogram), claims its
+//                     share of every bucket with one global atomic per (workgroup, bucket) and places its tiles there;
+//                     the last workgroup to finish clears the histogram and the claims for the next sort.
+// Within a bucket the order is not tile-index order (it depends on which workgroup claims first): no result depends on
+// the order (tiles are independent), only the drain tail.  The order is a permutation of the tiles whenever the costs
+// hold still during the sort (the runtime sorts a stream's own costs on that stream); HG_CHECK_EXEC builds also verify
+// that (hg_order_verify) and count every placement out of range into hg_counters.order_faults.
+struct HgOrderScratch {  // per trace stream, zeroed at allocation; every sort leaves it zeroed again
+    uint32_t hist[1024];   // tiles per bucket
+    uint32_t claim[1024];  // tiles per bucket claimed by workgroups so far
+    uint32_t done;         // workgroups of the scatter launch finished
+    uint32_t pad[31];
+};
+static_assert(sizeof(HgOrderScratch) == 8320, "order scratch");
+constexpr uint32_t kOrderTilesPerGroup = 1024;
+
+__device__ __forceinline__ uint32_t order_bucket(unsigned long long c) {
+    if (c < 2ull) return 1023u;
+    const uint32_t e = 63u - uint32_t(__builtin_clzll(c));                          // 1..63
+    const uint32_t m = uint32_t(e >= 4u ? (c >> (e - 4u)) : (c << (4u - e))) & 15u;  // the 4 bits after the leading 1
+    return 1023u - (e * 16u + m);
+}
+
+__global__ __launch_bounds__(64) void hg_order_hist(const unsigned long long* __restrict__ cost, uint32_t n,
+                                                    HgOrderScratch* __restrict__ sc) {
+    __shared__ uint32_t h[1024];
+    const uint32_t t = threadIdx.x, base = blockIdx.x * kOrderTilesPerGroup;
+    for (uint32_t b = t; b < 1024u; b += 64u) h[b] = 0u;
     __syncthreads();
-    unsigned long long m = 0;
-    for (uint32_t i = t; i < n; i += 1024) m = max(m, cost[i]);
-    atomicMax(&cmax, m);
+    for (uint32_t k = t; k < kOrderTilesPerGroup && base + k < n; k += 64u) atomicAdd(&h[order_bucket(cost[base + k])], 1u);
     __syncthreads();
-    const unsigned long long top = cmax;
-    // bucket = B-1 - floor(c * B / (top + 1)) for B = HG_ORDER_BUCKETS <= 1024, in 128-bit-safe form (c <= top);
-    // within a bucket the tiles keep their index order
-    auto bucket = [top](unsigned long long c) -> uint32_t {
-        constexpr uint32_t B = HG_ORDER_BUCKETS;
-        static_assert(B >= 1 && B <= 1024, "order buckets");
-        const unsigned long long q = top / B + 1u;  // c / q < B for every c <= top
-        return B - 1u - uint32_t((c < top ? c : top) / q);  // (the clamp only guards: costs must not change meanwhile)
-    };
-    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&start[bucket(cost[i])], 1u);
-    __syncthreads();
-    if (t == 0) {  // exclusive prefix sum over the buckets
-        uint32_t run = 0;
-        for (uint32_t b = 0; b < 1024u; ++b) {
-            const uint32_t k = start[b];
-            start[b] = run;
-            run += k;
-        }
+    for (uint32_t b = t; b < 1024u; b += 64u)
+        if (h[b]) atomicAdd(&sc->hist[b], h[b]);
+}
+
+__global__ __launch_bounds__(64) void hg_order_scatter(unsigned long long* __restrict__ cost, uint32_t* __restrict__ order,
+                                                       uint32_t n, HgOrderScratch* __restrict__ sc,
+                                                       unsigned long long* __restrict__ faults) {
+    __shared__ uint32_t pos[1024];  // bucket -> next place of this workgroup's tiles
+    __shared__ uint32_t cnt[1024];  // bucket -> this workgroup's tiles
+    const uint32_t t = threadIdx.x, base = blockIdx.x * kOrderTilesPerGroup;
+    // exclusive prefix of the global histogram: lane t sums buckets [16t, 16t + 16), a wave scan of the 64 sums
+    uint32_t run = 0;
+    for (uint32_t j = 0; j < 16u; ++j) {
+        const uint32_t v = __hip_atomic_load(&sc->hist[16u * t + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pos[16u * t + j] = run;
+        run += v;
+    }
+    uint32_t incl = run;
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (t >= d) incl += o;
+    }
+    const uint32_t excl = incl - run;
+    for (uint32_t j = 0; j < 16u; ++j) {
+        pos[16u * t + j] += excl;
+        cnt[16u * t + j] = 0u;
     }
     __syncthreads();
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    for (uint32_t base = 0; base < n; base += 1024u) {
-        const uint32_t i = base + t;
-        const bool valid = i < n;
-        const uint32_t b = valid ? bucket(cost[i]) : 1024u;  // 1024 (bit 10): past the end, no bucket
-        uint64_t same = ~0ull;
-        for (int bit = 0; bit < 11; ++bit) {  // lanes of this wave with the same bucket
-            const uint64_t set = __ballot((b >> bit) & 1u);
-            same &= ((b >> bit) & 1u) ? set : ~set;
+    for (uint32_t k = t; k < kOrderTilesPerGroup && base + k < n; k += 64u) atomicAdd(&cnt[order_bucket(cost[base + k])], 1u);
+    __syncthreads();
+    for (uint32_t b = t; b < 1024u; b += 64u)  // this workgroup's share of bucket b
+        if (cnt[b]) pos[b] += atomicAdd(&sc->claim[b], cnt[b]);
+    __syncthreads();
+    uint32_t bad = 0;
+    for (uint32_t k = t; k < kOrderTilesPerGroup && base + k < n; k += 64u) {
+        const uint32_t i = base + k;
+        const uint32_t p = atomicAdd(&pos[order_bucket(cost[i])], 1u);
+        if (p < n) order[p] = i;  // always, while the costs hold still during the sort
+        else ++bad;
+        cost[i] = 0ull;
+    }
+#if HG_CHECK_EXEC
+    if (bad && faults) atomicAdd(faults, (unsigned long long)bad);
+#else
+    (void)bad;
+    (void)faults;
+#endif
+    __syncthreads();
+    // the last workgroup out clears the histogram and the claims (every other one has read them: release / acquire)
+    uint32_t last = 0;
+    if (t == 0)
+        last = __hip_atomic_fetch_add(&sc->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (last) {
+        for (uint32_t b = t; b < 1024u; b += 64u) {
+            __hip_atomic_store(&sc->hist[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sc->claim[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const uint32_t rank = uint32_t(__popcll(same & lt_mask));
-        for (uint32_t w = 0; w < 16u; ++w) wcount[w][t] = 0;
-        __syncthreads();
-        if (valid && rank == 0) wcount[wave][b] = uint16_t(__popcll(same));
-        __syncthreads();
-        uint32_t run = 0;  // thread t = bucket t: exclusive prefix of its counts over the chunk's waves
-        for (uint32_t w = 0; w < 16u; ++w) {
-            const uint32_t k = wcount[w][t];
-            wcount[w][t] = uint16_t(run);
-            run += k;
-        }
-        __syncthreads();
-        if (valid) {
-            const uint32_t pos = start[b] + wcount[wave][b] + rank;
-            if (pos < n) order[pos] = i;  // always true while the costs hold still during the sort (the caller's duty)
-            cost[i] = 0;
-        }
-        __syncthreads();
-        start[t] += run;
-        __syncthreads();
+        if (t == 0) __hip_atomic_store(&sc->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, hipStream_t stream) {
+#if HG_CHECK_EXEC
+// HG_CHECK_EXEC builds: the order must be a permutation of [0, n).  seen[] (n words, zero) counts each tile's places;
+// the second kernel counts tiles placed other than once into *faults and zeroes seen[] again.
+__global__ __launch_bounds__(64) void hg_order_verify_mark(const uint32_t* __restrict__ order, uint32_t n,
+                                                           uint32_t* __restrict__ seen,
+                                                           unsigned long long* __restrict__ faults) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = order[i];
+    if (v < n) atomicAdd(&seen[v], 1u);
+    else atomicAdd(faults, 1ull);
+}
+__global__ __launch_bounds__(64) void hg_order_verify_count(uint32_t n, uint32_t* __restrict__ seen,
+                                                            unsigned long long* __restrict__ faults) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    if (seen[i] != 1u) atomicAdd(faults, 1ull);
+    seen[i] = 0u;
+}
+#endif
+
+size_t hg_order_scratch_bytes(uint32_t n) {
+    return sizeof(HgOrderScratch) + (HG_CHECK_EXEC ? size_t(n) * sizeof(uint32_t) : 0);
+}
+
+// scratch: hg_order_scratch_bytes(n) bytes, zeroed when allocated; faults: hg_counters.order_faults (check builds)
+hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, void* scratch,
+                                 unsigned long long* faults, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(hg_order_tiles, dim3(1), dim3(1024), 0, stream, cost, order, n);
+    HgOrderScratch* sc = static_cast<HgOrderScratch*>(scratch);
+    const dim3 g{(n + kOrderTilesPerGroup - 1) / kOrderTilesPerGroup};
+    hipLaunchKernelGGL(hg_order_hist, g, dim3(64), 0, stream, cost, n, sc);
+    hipLaunchKernelGGL(hg_order_scatter, g, dim3(64), 0, stream, cost, order, n, sc, faults);
+#if HG_CHECK_EXEC
+    uint32_t* seen = reinterpret_cast<uint32_t*>(sc + 1);
+    hipLaunchKernelGGL(hg_order_verify_mark, dim3((n + 63) / 64), dim3(64), 0, stream, order, n, seen, faults);
+    hipLaunchKernelGGL(hg_order_verify_count, dim3((n + 63) / 64), dim3(64), 0, stream, n, seen, faults);
+#endif
     return hipGetLastError();
 }
 
@@ -418,7 +478,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
                     const size_t slot_i = size_t(uint32_t(local_tile)) * 64u + pix;
-                    if (HG_REGEN_ITEMS || split > 1u) {  // this frame's colour, blended later in frame order
+                    // this frame's colour, blended later in frame order: every launch of the trace pipeline (the runtime
+                    // passes a colour buffer exactly then, and blends after every chunk of it, a 1-frame chunk included)
+                    if (HG_REGEN_ITEMS || kp.frame_color != nullptr) {
                         fc_store(kp.frame_color + fc_index(kp, fs >> 16, slot_i),
                                  make_float4(color.x, color.y, color.z, 1.0f));
                     } else {
@@ -1034,6 +1096,21 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         if (kCounters) cyc_shade += wave_clock();
     }
     record_tile_cost(lane);
+    if constexpr (kQueue) {
+        // The last wave out resets the queue heads for the next launch on this stream (no memset launch per queue
+        // launch: a blit kernel waited for a CU that the other streams' persistent waves held).  A wave leaves only
+        // once its pulls found the queue dry, and it pulls no more after that: every head access of the launch
+        // happens before the last wave's increment of the exit count (release / acquire).
+        if (lane == 0u) {
+            const uint32_t out = __hip_atomic_fetch_add(kp.queue + HG_QUEUE_DONE_WORD, 1u, __ATOMIC_ACQ_REL,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (out == gridDim.x - 1u) {
+                for (uint32_t h = 0; h < 8u; ++h)
+                    __hip_atomic_store(kp.queue + 32u * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(kp.queue + HG_QUEUE_DONE_WORD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     if (kCounters) {
         const uint32_t v[9] = {paths, c.rays, c.tri, c.aabb, c.rays * nm, c.rays * uint32_t(kp.n_spheres), c.hits,
                                c.node_rounds, c.tri_rounds};

@@ -20,12 +20,15 @@
 #include "hg_layout.h"
 #include "hg_ctx.h"
 #include "hg_tiling.h"
+#include "hg_interval.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
-hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, hipStream_t stream);
+hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, void* scratch,
+                                 unsigned long long* faults, hipStream_t stream);
+size_t hg_order_scratch_bytes(uint32_t n);
 #ifndef HG_WITH_VARIANTS
 #define HG_WITH_VARIANTS 0  // A/B variants (wavefront pipeline, path pool): make VARIANTS=1
 #endif
@@ -258,8 +261,9 @@ int drain_events(hg_ctx* c) {
         c->counters.kernel_ms += double(ms);
         c->free_events.push_back(pr);
     }
-    // the launches' intervals relative to the first start (the trace streams' events share the device clock); the
-    // batch ends at a synchronisation, so batches do not overlap one another
+    // the launches' intervals relative to the first one pushed (which need not be the first to start: offsets can be
+    // negative; the trace streams' events share the device clock); the batch ends at a synchronisation, so batches do
+    // not overlap one another
     std::vector<std::pair<double, double>> iv;
     iv.reserve(c->pending_trace.size());
     for (auto& pr : c->pending_trace) {
@@ -270,18 +274,7 @@ int drain_events(hg_ctx* c) {
         c->counters.trace_ms += double(ms);
         c->counters.trace_launches++;
     }
-    std::sort(iv.begin(), iv.end());
-    double covered = 0.0, lo = 0.0, hi = -1.0;
-    for (const auto& x : iv) {
-        if (x.first > hi) {
-            if (hi > lo) covered += hi - lo;
-            lo = x.first;
-            hi = x.second;
-        } else if (x.second > hi) {
-            hi = x.second;
-        }
-    }
-    if (hi > lo) covered += hi - lo;
+    const double covered = hg_interval_union(std::move(iv));
     c->counters.trace_busy_ms += covered;
     for (auto& pr : c->pending_trace) c->free_events.push_back(pr);
     c->pending.clear();
@@ -512,7 +505,7 @@ int hg_create(int device, hg_ctx** out) {
 
 void hg_destroy(hg_ctx* c) {
     if (!c) return;
-    (void)hg_ctx_flush(c);
+    c->pending_frames = 0;  // held frames are discarded: nothing can observe them after this call
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (hg_ctx::TraceLane& L : c->lanes)
@@ -523,7 +516,8 @@ void hg_destroy(hg_ctx* c) {
                       &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->pool})
         release(*b);
     for (hg_ctx::TraceLane& L : c->lanes) {
-        for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.queue}) release(*b);
+        for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.order_scratch, &L.queue})
+            release(*b);
         if (L.traced) (void)hipEventDestroy(L.traced);
         if (L.blended) (void)hipEventDestroy(L.blended);
         if (L.stream) (void)hipStreamDestroy(L.stream);
@@ -1011,7 +1005,18 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 if (!rc && spill_bytes) rc = ensure_quiet(c, L.spill, spill_bytes);
                 if (!rc && ordered) rc = ensure_quiet(c, L.tile_cost, 2 * tb);
                 if (!rc && ordered) rc = ensure_quiet(c, L.tile_order, tb);
-                if (!rc && stream_k) rc = ensure_quiet(c, L.queue, 8 * 128);
+                // the sort's scratch and the queue heads are zeroed once, when allocated (each use leaves them zeroed)
+                const size_t osb = hg_order_scratch_bytes(uint32_t(tiles));
+                if (!rc && ordered && L.order_scratch.bytes < osb) {
+                    rc = ensure_quiet(c, L.order_scratch, osb);
+                    if (!rc && hipMemsetAsync(L.order_scratch.p, 0, L.order_scratch.bytes, L.stream) != hipSuccess)
+                        rc = fail(c, HG_E_HIP, "hipMemsetAsync(order scratch) failed");
+                }
+                if (!rc && stream_k && L.queue.bytes < HG_QUEUE_BYTES) {
+                    rc = ensure_quiet(c, L.queue, HG_QUEUE_BYTES);
+                    if (!rc && hipMemsetAsync(L.queue.p, 0, L.queue.bytes, L.stream) != hipSuccess)
+                        rc = fail(c, HG_E_HIP, "hipMemsetAsync(queue) failed");
+                }
                 if (rc) {
                     c->free_events.push_back(ev);
                     return rc;
@@ -1064,7 +1069,8 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     if (L.tile_cost_valid &&
                         (!L.tile_order_valid || L.frames_since_order >= int64_t(HG_ORDER_MIN_FRAMES))) {
                         e = hg_launch_order_tiles(kc.tile_cost, static_cast<uint32_t*>(L.tile_order.p), uint32_t(tiles),
-                                                  L.stream);
+                                                  L.order_scratch.p,
+                                                  static_cast<unsigned long long*>(c->counters_dev.p) + 18, L.stream);
                         L.tile_order_valid = e == hipSuccess;
                         L.frames_since_order = 0;
                     } else if (!L.tile_cost_valid) {
@@ -1076,7 +1082,6 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     L.tile_cost_valid = e == hipSuccess;
                     L.frames_since_order += kc.n_frames;
                 }
-                if (e == hipSuccess && kc.queue) e = hipMemsetAsync(kc.queue, 0, 8 * 128, L.stream);
                 std::pair<hipEvent_t, hipEvent_t> tev{};
                 if (e == hipSuccess && c->timing) {
                     if (int rc = event_pair(c, tev)) {
@@ -1342,6 +1347,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->shade_rounds = v[15];
     out->primary_misses = v[16];
     out->exec_fallbacks = v[17];
+    out->order_faults = v[18];
     return HG_OK;
 }
 
@@ -1361,7 +1367,7 @@ int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
     if (int rc = set_device(c)) return rc;
     if (test == HG_SELFTEST_BUILD) {  // compile-time checks of this build (no device work)
         if (tested) *tested = 0;
-        return HG_CHECK_EXEC ? HG_BUILD_CHECK_EXEC : 0;
+        return (HG_CHECK_EXEC ? HG_BUILD_CHECK_EXEC : 0) | (HG_REGEN_ITEMS ? 0 : HG_BUILD_NO_REGEN_ITEMS);
     }
     if (test != HG_SELFTEST_RCP) return fail(c, HG_E_INVALID, "unknown self-test %d", test);
     const int64_t r = hg_selftest_rcp_all(tested);

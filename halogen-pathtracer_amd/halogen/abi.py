@@ -82,7 +82,7 @@ class HgCounters(C.Structure):
                 ("tri_rounds", C.c_uint64), ("last_kernel", C.c_uint64),
                 ("trace_cycles", C.c_uint64), ("shade_cycles", C.c_uint64),
                 ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64),
-                ("exec_fallbacks", C.c_uint64), ("trace_busy_ms", C.c_double)]
+                ("exec_fallbacks", C.c_uint64), ("trace_busy_ms", C.c_double), ("order_faults", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)
@@ -112,6 +112,7 @@ HG_COMM_RCCL, HG_COMM_PEER = 1, 2
 HG_SELFTEST_RCP = 1
 HG_SELFTEST_BUILD = 2
 HG_BUILD_CHECK_EXEC = 1
+HG_BUILD_NO_REGEN_ITEMS = 2
 
 _lib = None
 

@@ -25,6 +25,10 @@
  *   - host arrays are copied during the call (SetBufferData semantics); counts of 0 are legal.
  *   - one context = one device + one HIP stream; a context is NOT thread-safe; one context per GPU may be
  *     driven from separate host threads.  hg_render is asynchronous; hg_readback / hg_synchronize block.
+ *   - held frames (HG_OPT_COALESCE): hg_render may hold its frames and launch them with later calls; every other entry
+ *     point launches the held frames first.  A launch that fails there (out of memory, a HIP error) is reported by
+ *     THAT entry point, with the text of the failed launch, and the held frames are lost (FrameCount does not advance
+ *     for them).  hg_destroy discards held frames without launching them.
  *   - no torch / HIP types appear in any signature.
  */
 #ifndef HALOGEN_ABI_H
@@ -162,6 +166,9 @@ typedef struct hg_counters {
     double trace_busy_ms;  /* the union of the traversal kernel's timed launch intervals (HG_OPT_TIMING): launches on the
                               two trace streams overlap, so trace_ms counts shared time twice; trace_busy_ms /
                               trace_launches is the kernel's device time per launch */
+    uint64_t order_faults; /* HG_CHECK_EXEC builds only: cost-order sorts whose output was not a permutation of the tiles
+                              (a placement out of range, or a tile placed other than once); must stay 0.  0 in product
+                              builds */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -291,8 +298,10 @@ int hg_set_option(hg_ctx* ctx, int32_t option, int32_t value);
  * reciprocal against IEEE 1.0f/x for every float of its range.  Returns the number of mismatches (must be 0),
  * or a negative error; *tested (optional) receives the number of inputs checked. */
 enum { HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2 };
-/* HG_SELFTEST_BUILD returns a bit mask of the run-time checks compiled into this build (no device work). */
-enum { HG_BUILD_CHECK_EXEC = 1 };
+/* HG_SELFTEST_BUILD returns a bit mask of the run-time checks and A/B switches compiled into this build (no device
+ * work): HG_BUILD_CHECK_EXEC, the run-time precondition checks (make check_exec); HG_BUILD_NO_REGEN_ITEMS, the
+ * regenerating kernel without (pixel, frame) item scheduling (make noitems). */
+enum { HG_BUILD_CHECK_EXEC = 1, HG_BUILD_NO_REGEN_ITEMS = 2 };
 int64_t hg_selftest(hg_ctx* ctx, int32_t test, int64_t* tested);
 
 /* ----------------------------------------------------------------------------------------------
