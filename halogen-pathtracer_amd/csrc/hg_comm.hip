@@ -170,14 +170,22 @@ int wait_comms_ready(hg_comm* m, const char* what) {
 
 // Wait for every member stream to drain.  The deadline starts once each member's `ready` event (recorded ahead of its
 // RCCL work) has completed, i.e. once this process's own renders are done; RCCL errors are polled throughout.
-int wait_streams(hg_comm* m, const char* what) {
+// Wait until every member stream is idle (until_event == nullptr) or until `until_event` (an event on the root
+// context's stream) has completed, bounded as hg_comm_synchronize documents.
+int wait_streams(hg_comm* m, const char* what, hipEvent_t until_event = nullptr) {
     bool armed = m->transport != HG_COMM_RCCL;  // the peer transport has no remote party: plain deadline
     auto deadline = Clock::now() + std::chrono::milliseconds(m->timeout_ms);
     for (;;) {
         bool all_done = true, all_ready = true;
+        if (until_event) {
+            HG_CHIP(m, hipSetDevice(m->root_ctx->device));
+            const hipError_t e = hipEventQuery(until_event);
+            if (e == hipErrorNotReady) all_done = false;
+            else if (e != hipSuccess) return cfail(m, HG_E_HIP, "%s: %s", what, hipGetErrorString(e));
+        }
         for (auto& mb : m->members) {
             HG_CHIP(m, hipSetDevice(mb.ctx->device));
-            const hipError_t e = hipStreamQuery(mb.ctx->stream);
+            const hipError_t e = until_event ? hipSuccess : hipStreamQuery(mb.ctx->stream);
             if (e == hipErrorNotReady) {
                 all_done = false;
             } else if (e != hipSuccess) {
@@ -591,6 +599,32 @@ int hg_comm_readback(hg_comm* m, float* rgba, size_t n_floats) {
     HG_CHIP(m, hipMemcpyAsync(rgba, m->image.p, size_t(m->W) * size_t(m->H) * sizeof(float4), hipMemcpyDeviceToHost,
                               rc->stream));
     HG_CHIP(m, hipStreamSynchronize(rc->stream));
+    return HG_OK;
+}
+
+// Pipelined display of the gathered image (the multi-GPU form of hg_readback_begin_format / hg_readback_end_data):
+// enqueued on the root context's stream after the last gather's assembly, into that context's ring of pinned host
+// images (HG_OPT_READBACK_DEPTH of the root context); the end waits for the oldest one with the deadline of
+// hg_comm_synchronize, so a dead peer cannot hang the display.
+int hg_comm_readback_begin(hg_comm* m, int32_t format) {
+    if (!m) return HG_E_INVALID;
+    if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
+    if (m->root < 0 || !m->root_ctx) return cfail(m, HG_E_INVALID, "no gathered image in this process");
+    hg_ctx* rc = m->root_ctx;
+    if (rc->W != m->W || rc->H != m->H) return cfail(m, HG_E_INVALID, "the root context was resized after the gather");
+    if (int e = hg_ctx_display_begin(rc, m->image.p, format)) return cfail(m, e, "%s", rc->err.c_str());
+    return HG_OK;
+}
+
+int hg_comm_readback_end(hg_comm* m, const void** data, size_t* n_bytes, int32_t* format) {
+    if (!m || !data) return HG_E_INVALID;
+    if (m->aborted) return cfail(m, HG_E_COMM, "communicator was aborted after an earlier failure");
+    if (!m->root_ctx) return cfail(m, HG_E_INVALID, "no gathered image in this process");
+    hipEvent_t ev = hg_ctx_display_oldest(m->root_ctx);
+    if (!ev) return cfail(m, HG_E_INVALID, "no readback outstanding: call hg_comm_readback_begin first");
+    if (int rc = wait_streams(m, "hg_comm_readback_end", ev)) return rc;
+    if (int e = hg_readback_end_data(m->root_ctx, data, n_bytes, format))
+        return cfail(m, e, "%s", m->root_ctx->err.c_str());
     return HG_OK;
 }
 

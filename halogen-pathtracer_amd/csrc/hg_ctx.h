@@ -94,14 +94,21 @@ struct hg_ctx {
     int32_t coalesce = HG_COALESCE;
     int32_t pending_frames = 0, pending_acc = 0;
 
-    // Display readback (hg_readback, hg_readback_begin / _end): the accumulator untiled on the device into `image`
-    // (row-major float4), then copied into one of two pinned host images
+    // Display readback (hg_readback, hg_readback_begin[_format] / _end[_data]): the accumulator untiled on the device
+    // into `image` (row-major, in the display format), then copied into the next of rb_depth pinned host images (a ring)
     DevBuf image;
-    float* image_host[2] = {nullptr, nullptr};
-    size_t image_host_bytes = 0;
-    hipEvent_t image_copied[2] = {nullptr, nullptr};
-    int rb_next = 0, rb_pending = 0;  // host image the next begin fills; begun readbacks not yet ended (<= 2)
+    void* image_host[HG_READBACK_MAX] = {};
+    size_t image_host_cap[HG_READBACK_MAX] = {};    // allocated bytes
+    size_t image_host_bytes[HG_READBACK_MAX] = {};  // bytes of the readback it holds
+    int32_t image_host_format[HG_READBACK_MAX] = {};
+    hipEvent_t image_copied[HG_READBACK_MAX] = {};
+    int rb_depth = 2;                 // HG_OPT_READBACK_DEPTH: readbacks that may be outstanding
+    int rb_next = 0, rb_pending = 0;  // host image the next begin fills; begun readbacks not yet ended (<= rb_depth)
 };
 
 // Launch the held frames of a context, if any (hg_runtime.hip; every entry point but hg_render calls it first)
 int hg_ctx_flush(hg_ctx* c);
+// Enqueue a display readback (hg_readback_begin_format) from the accumulator (rows == nullptr) or from a row-major
+// float4 image of the target's size on the context's device; and the copy event of the oldest outstanding one
+int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format);
+hipEvent_t hg_ctx_display_oldest(const hg_ctx* c);

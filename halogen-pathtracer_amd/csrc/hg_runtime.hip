@@ -21,6 +21,7 @@
 #include "hg_ctx.h"
 #include "hg_tiling.h"
 #include "hg_interval.h"
+#include "hg_pack.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
@@ -345,6 +346,7 @@ int alloc_target(hg_ctx* c) {
     (void)slots;
 #endif
     c->rb_pending = 0;  // quiesced: begun readbacks are complete, and their images die with the old size or tiling
+    c->rb_next = 0;
     release(c->acc);
     if (bytes) {
         hipError_t e = hipMalloc(&c->acc.p, bytes);
@@ -523,7 +525,7 @@ void hg_destroy(hg_ctx* c) {
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
     release(c->image);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < HG_READBACK_MAX; ++k) {
         if (c->image_host[k]) (void)hipHostFree(c->image_host[k]);
         if (c->image_copied[k]) (void)hipEventDestroy(c->image_copied[k]);
     }
@@ -1148,78 +1150,160 @@ int hg_ctx_flush(hg_ctx* c) {
     return render_now(c, n, acc);
 }
 
-// The accumulator (this rank's tiles, tile-major) as a row-major image; pixels of other ranks' tiles are 0.  One thread
-// per pixel: the stores are contiguous, the loads are 8 consecutive float4 per tile row.
-__global__ __launch_bounds__(256) void hg_untile_image(float4* __restrict__ image, const float4* __restrict__ acc,
+// The accumulator (this rank's tiles, tile-major) as a row-major image in a display format (hg_pack.h); pixels of
+// other ranks' tiles are 0.  One thread per pixel: the stores are contiguous (16 / 8 / 4 B per pixel), the loads are 8
+// consecutive float4 per tile row.
+template <int kFmt, bool kRows>
+__global__ __launch_bounds__(256) void hg_untile_image(void* __restrict__ image, const float4* __restrict__ acc,
                                                        int32_t W, int32_t H, int32_t tiles_x, int32_t rank,
                                                        int32_t n_ranks) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= uint32_t(W) * uint32_t(H)) return;
-    const HgPixelSource s = hg_pixel_source(i % uint32_t(W), i / uint32_t(W), uint32_t(tiles_x), uint32_t(n_ranks));
-    image[i] = s.rank == uint32_t(rank) ? acc[size_t(s.local_tile) * 64u + s.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v;
+    if constexpr (kRows) {  // the source is already a row-major image (the multi-GPU gather's assembled image)
+        v = acc[i];
+    } else {
+        const HgPixelSource s = hg_pixel_source(i % uint32_t(W), i / uint32_t(W), uint32_t(tiles_x), uint32_t(n_ranks));
+        v = s.rank == uint32_t(rank) ? acc[size_t(s.local_tile) * 64u + s.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (kFmt == HG_DISPLAY_RGBA32F) {
+        static_cast<float4*>(image)[i] = v;
+    } else if constexpr (kFmt == HG_DISPLAY_RGBA16F) {
+        uint32_t h[2];
+        hg_pack_rgba16f(v.x, v.y, v.z, v.w, h);
+        static_cast<uint2*>(image)[i] = make_uint2(h[0], h[1]);
+    } else {
+        static_cast<uint32_t*>(image)[i] = hg_pack_r11g11b10(v.x, v.y, v.z);
+    }
 }
 
 namespace {
 
-// Enqueue on the context stream: untile the accumulator into c->image (grown as needed).  Returns its size in bytes.
-int untile_async(hg_ctx* c, size_t* bytes) {
+size_t display_bpp(int32_t format) {
+    return format == HG_DISPLAY_RGBA32F ? 16 : format == HG_DISPLAY_RGBA16F ? 8 : format == HG_DISPLAY_R11G11B10F ? 4 : 0;
+}
+
+template <bool kRows>
+void launch_untile(hg_ctx* c, int32_t format, const float4* src) {
     const size_t pixels = size_t(c->W) * size_t(c->H);
-    *bytes = pixels * sizeof(float4);
+    const dim3 g(uint32_t((pixels + 255) / 256)), b(256);
+    if (format == HG_DISPLAY_RGBA16F)
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA16F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
+                           c->H, c->tiles_x, c->rank, c->n_ranks);
+    else if (format == HG_DISPLAY_R11G11B10F)
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_R11G11B10F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
+                           c->H, c->tiles_x, c->rank, c->n_ranks);
+    else
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA32F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
+                           c->H, c->tiles_x, c->rank, c->n_ranks);
+}
+
+// Enqueue on the context stream: the accumulator untiled (or, with `rows`, a row-major float4 image of the target's
+// size converted) into c->image (grown as needed) in `format`.  Returns its size in bytes.
+int untile_async(hg_ctx* c, size_t* bytes, int32_t format = HG_DISPLAY_RGBA32F, const float4* rows = nullptr) {
+    const size_t pixels = size_t(c->W) * size_t(c->H);
+    *bytes = pixels * display_bpp(format);
     if (c->image.bytes < *bytes) {  // everything that might read the old image is ordered before on the context stream
         HG_HIP(c, hipStreamSynchronize(c->stream));
         if (int rc = ensure(c, c->image, *bytes)) return rc;
     }
-    hipLaunchKernelGGL(hg_untile_image, dim3(uint32_t((pixels + 255) / 256)), dim3(256), 0, c->stream,
-                       static_cast<float4*>(c->image.p), static_cast<const float4*>(c->acc.p), c->W, c->H, c->tiles_x,
-                       c->rank, c->n_ranks);
+    if (rows) launch_untile<true>(c, format, rows);
+    else launch_untile<false>(c, format, static_cast<const float4*>(c->acc.p));
     HG_HIP(c, hipGetLastError());
     return HG_OK;
 }
 
 }  // namespace
 
-extern "C" {
-
-int hg_readback_begin(hg_ctx* c) {
-    if (!c) return HG_E_INVALID;
+// The display readback of hg_readback_begin_format, from the accumulator (rows == nullptr) or from a row-major float4
+// image of the target's size on the context's device (the comm's assembled image, hg_comm_readback_begin)
+int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
     if (int rc = hg_ctx_flush(c)) return rc;
     if (c->W <= 0) return fail(c, HG_E_NOTARGET, "hg_resize not called");
-    if (c->rb_pending >= 2) return fail(c, HG_E_INVALID, "two readbacks outstanding: call hg_readback_end first");
+    if (!display_bpp(format)) return fail(c, HG_E_INVALID, "unknown display format %d", format);
+    if (c->rb_pending >= c->rb_depth)
+        return fail(c, HG_E_INVALID, "%d readbacks outstanding (HG_OPT_READBACK_DEPTH): call hg_readback_end first",
+                    c->rb_pending);
     if (int rc = set_device(c)) return rc;
     size_t bytes = 0;
-    if (int rc = untile_async(c, &bytes)) return rc;
-    if (c->image_host_bytes != bytes) {  // (re)size both host images; none is outstanding (rb_pending counts them)
-        if (c->rb_pending) HG_HIP(c, hipStreamSynchronize(c->stream));
-        for (int k = 0; k < 2; ++k) {
-            if (c->image_host[k]) HG_HIP(c, hipHostFree(c->image_host[k]));
-            c->image_host[k] = nullptr;
+    if (int rc = untile_async(c, &bytes, format, static_cast<const float4*>(rows))) return rc;
+    const int k = c->rb_next;  // not outstanding: at most rb_depth are, and k is the slot after the newest
+    if (c->image_host_cap[k] < bytes) {
+        if (c->image_host[k]) {
+            HG_HIP(c, hipEventSynchronize(c->image_copied[k]));  // (its last copy was ended, so this returns at once)
+            HG_HIP(c, hipHostFree(c->image_host[k]));
         }
-        c->image_host_bytes = 0;
-        for (int k = 0; k < 2; ++k) {
-            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->image_host[k]), bytes, 0);
-            if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-            if (!c->image_copied[k]) HG_HIP(c, hipEventCreateWithFlags(&c->image_copied[k], hipEventDisableTiming));
-        }
-        c->image_host_bytes = bytes;
-        c->rb_pending = 0;
+        c->image_host[k] = nullptr;
+        c->image_host_cap[k] = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->image_host[k]), bytes, 0);
+        if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        c->image_host_cap[k] = bytes;
+        if (!c->image_copied[k]) HG_HIP(c, hipEventCreateWithFlags(&c->image_copied[k], hipEventDisableTiming));
     }
-    const int k = c->rb_next;
     HG_HIP(c, hipMemcpyAsync(c->image_host[k], c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HG_HIP(c, hipEventRecord(c->image_copied[k], c->stream));
-    c->rb_next = k ^ 1;
+    c->image_host_bytes[k] = bytes;
+    c->image_host_format[k] = format;
+    c->rb_next = (k + 1) % c->rb_depth;
     c->rb_pending++;
+    return HG_OK;
+}
+
+// The copy event of the oldest outstanding display readback (nullptr when none is outstanding)
+hipEvent_t hg_ctx_display_oldest(const hg_ctx* c) {
+    if (c->rb_pending <= 0) return nullptr;
+    return c->image_copied[(c->rb_next - c->rb_pending + c->rb_depth) % c->rb_depth];
+}
+
+extern "C" {
+
+int hg_readback_begin_format(hg_ctx* c, int32_t format) {
+    if (!c) return HG_E_INVALID;
+    return hg_ctx_display_begin(c, nullptr, format);
+}
+
+int hg_readback_begin(hg_ctx* c) { return hg_readback_begin_format(c, HG_DISPLAY_RGBA32F); }
+
+int hg_readback_end_data(hg_ctx* c, const void** data, size_t* n_bytes, int32_t* format) {
+    if (!c || !data) return HG_E_INVALID;
+    if (c->rb_pending <= 0) return fail(c, HG_E_INVALID, "no readback outstanding: call hg_readback_begin first");
+    if (int rc = set_device(c)) return rc;
+    const int k = (c->rb_next - c->rb_pending + c->rb_depth) % c->rb_depth;  // the oldest begun
+    HG_HIP(c, hipEventSynchronize(c->image_copied[k]));
+    c->rb_pending--;
+    *data = c->image_host[k];
+    if (n_bytes) *n_bytes = c->image_host_bytes[k];
+    if (format) *format = c->image_host_format[k];
     return HG_OK;
 }
 
 int hg_readback_end(hg_ctx* c, const float** rgba, size_t* n_floats) {
     if (!c || !rgba) return HG_E_INVALID;
     if (c->rb_pending <= 0) return fail(c, HG_E_INVALID, "no readback outstanding: call hg_readback_begin first");
-    if (int rc = set_device(c)) return rc;
-    const int k = c->rb_pending == 2 ? c->rb_next : c->rb_next ^ 1;  // the oldest begun
-    HG_HIP(c, hipEventSynchronize(c->image_copied[k]));
-    c->rb_pending--;
-    *rgba = c->image_host[k];
-    if (n_floats) *n_floats = c->image_host_bytes / sizeof(float);
+    const int k = (c->rb_next - c->rb_pending + c->rb_depth) % c->rb_depth;
+    if (c->image_host_format[k] != HG_DISPLAY_RGBA32F)
+        return fail(c, HG_E_INVALID, "the oldest readback is in display format %d: use hg_readback_end_data",
+                    c->image_host_format[k]);
+    const void* data = nullptr;
+    size_t bytes = 0;
+    if (int rc = hg_readback_end_data(c, &data, &bytes, nullptr)) return rc;
+    *rgba = static_cast<const float*>(data);
+    if (n_floats) *n_floats = bytes / sizeof(float);
+    return HG_OK;
+}
+
+int hg_pack_display(const float* rgba, size_t n_pixels, int32_t format, void* out) {
+    if ((n_pixels && (!rgba || !out)) || !display_bpp(format)) return HG_E_INVALID;
+    for (size_t i = 0; i < n_pixels; ++i) {
+        const float* v = rgba + 4 * i;
+        if (format == HG_DISPLAY_RGBA32F) {
+            std::memcpy(static_cast<float*>(out) + 4 * i, v, 16);
+        } else if (format == HG_DISPLAY_RGBA16F) {
+            hg_pack_rgba16f(v[0], v[1], v[2], v[3], static_cast<uint32_t*>(out) + 2 * i);
+        } else {
+            static_cast<uint32_t*>(out)[i] = hg_pack_r11g11b10(v[0], v[1], v[2]);
+        }
+    }
     return HG_OK;
 }
 
@@ -1412,6 +1496,13 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_COALESCE:
             if (value < 1 || value > 65535) return fail(c, HG_E_INVALID, "coalesce window must be 1..65535 frames");
             c->coalesce = value;
+            return HG_OK;
+        case HG_OPT_READBACK_DEPTH:
+            if (value < 1 || value > HG_READBACK_MAX)
+                return fail(c, HG_E_INVALID, "readback depth must be 1..%d", HG_READBACK_MAX);
+            if (c->rb_pending) return fail(c, HG_E_INVALID, "readbacks outstanding: end them before changing the depth");
+            c->rb_depth = value;
+            c->rb_next = 0;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

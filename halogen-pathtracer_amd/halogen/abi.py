@@ -96,15 +96,22 @@ HG_OPT_KERNEL, HG_OPT_BLOCK, HG_OPT_COUNTERS, HG_OPT_TIMING, HG_OPT_REFILL, HG_O
 HG_OPT_DESCENT_T = 7
 HG_OPT_TILE_ORDER = 8
 HG_OPT_COALESCE = 9
+HG_OPT_READBACK_DEPTH = 10
+HG_READBACK_MAX = 8
+# display formats of readback_begin(format=...) (include/halogen_abi.h, csrc/hg_pack.h): bytes per pixel and numpy view
+HG_DISPLAY_RGBA32F, HG_DISPLAY_RGBA16F, HG_DISPLAY_R11G11B10F = 0, 1, 2
+DISPLAY_FORMATS = {"rgba32f": HG_DISPLAY_RGBA32F, "rgba16f": HG_DISPLAY_RGBA16F, "r11g11b10f": HG_DISPLAY_R11G11B10F}
+DISPLAY_BPP = {HG_DISPLAY_RGBA32F: 16, HG_DISPLAY_RGBA16F: 8, HG_DISPLAY_R11G11B10F: 4}
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [
     "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
-    "hg_readback", "hg_readback_begin", "hg_readback_end", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
+    "hg_readback", "hg_readback_begin", "hg_readback_end", "hg_readback_begin_format", "hg_readback_end_data",
+    "hg_pack_display", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
     "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
     "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_synchronize",
-    "hg_comm_readback", "hg_comm_set_timeout_ms", "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
+    "hg_comm_readback", "hg_comm_readback_begin", "hg_comm_readback_end", "hg_comm_set_timeout_ms", "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
     "hg_comm_assemble_host",
 ]
 HG_COMM_ID_BYTES = 128
@@ -143,6 +150,9 @@ def lib() -> C.CDLL:
         "hg_readback": (C.c_int, [P, f32p, sz]),
         "hg_readback_begin": (C.c_int, [P]),
         "hg_readback_end": (C.c_int, [P, C.POINTER(f32p), C.POINTER(sz)]),
+        "hg_readback_begin_format": (C.c_int, [P, i32]),
+        "hg_readback_end_data": (C.c_int, [P, C.POINTER(P), C.POINTER(sz), C.POINTER(i32)]),
+        "hg_pack_display": (C.c_int, [f32p, sz, i32, P]),
         "hg_set_accumulation": (C.c_int, [P, f32p, sz, i32]),
         "hg_copy_tiles_device": (C.c_int, [P, P, sz]),
         "hg_local_tile_count": (i32, [P]),
@@ -160,6 +170,8 @@ def lib() -> C.CDLL:
         "hg_comm_gather": (C.c_int, [P, i32]),
         "hg_comm_synchronize": (C.c_int, [P]),
         "hg_comm_readback": (C.c_int, [P, f32p, sz]),
+        "hg_comm_readback_begin": (C.c_int, [P, i32]),
+        "hg_comm_readback_end": (C.c_int, [P, C.POINTER(P), C.POINTER(sz), C.POINTER(i32)]),
         "hg_comm_set_timeout_ms": (C.c_int, [P, i64]),
         "hg_comm_assemble_host": (C.c_int, [f32p, i64, i32, i32, i32, f32p, sz]),
         "hg_comm_transport": (C.c_int, [P]),
@@ -190,6 +202,21 @@ def _ptr(a) -> C.c_void_p:
     if isinstance(a, np.ndarray):
         return C.c_void_p(a.ctypes.data)
     return C.cast(a, C.c_void_p)
+
+
+def _display_view(ptr: C.c_void_p, n_bytes: int, fmt: int, w: int, h: int, copy: bool) -> np.ndarray:
+    """A display image (hg_readback_end_data) as (h, w, 4) float32 / (h, w, 4) float16 / (h, w) uint32."""
+    bpp = DISPLAY_BPP.get(fmt)
+    if bpp is None or n_bytes != w * h * bpp:
+        raise HalogenError(f"display readback: {n_bytes} bytes of format {fmt} for a {w}x{h} target")
+    raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n_bytes,))
+    if fmt == HG_DISPLAY_RGBA32F:
+        view = raw.view(np.float32).reshape(h, w, 4)
+    elif fmt == HG_DISPLAY_RGBA16F:
+        view = raw.view(np.float16).reshape(h, w, 4)
+    else:
+        view = raw.view(np.uint32).reshape(h, w)
+    return view.copy() if copy else view
 
 
 def as_struct_array(struct_type, n: int):
@@ -266,19 +293,21 @@ class Context:
         self._check(lib().hg_readback(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size), "hg_readback")
         return out
 
-    def readback_begin(self) -> None:
-        """hg_readback_begin: enqueue the display readback of every frame rendered so far (at most 2 outstanding)."""
-        self._check(lib().hg_readback_begin(self._h), "hg_readback_begin")
+    def readback_begin(self, fmt: int | None = None) -> None:
+        """hg_readback_begin(_format): enqueue the display readback of every frame rendered so far (at most
+        HG_OPT_READBACK_DEPTH outstanding), as RGBA32F or another HG_DISPLAY_* format."""
+        if fmt is None:
+            self._check(lib().hg_readback_begin(self._h), "hg_readback_begin")
+        else:
+            self._check(lib().hg_readback_begin_format(self._h, int(fmt)), "hg_readback_begin_format")
 
     def readback_end(self, w: int, h: int, copy: bool = True) -> np.ndarray:
-        """hg_readback_end: the (h, w, 4) image of the oldest begun readback.  copy=False returns a view of the
-        context's pinned host image, valid until the second readback_begin after the one it came from."""
-        ptr, n = C.POINTER(C.c_float)(), C.c_size_t(0)
-        self._check(lib().hg_readback_end(self._h, C.byref(ptr), C.byref(n)), "hg_readback_end")
-        if n.value != w * h * 4:
-            raise HalogenError(f"hg_readback_end: {n.value} floats for a {w}x{h} target")
-        view = np.ctypeslib.as_array(ptr, shape=(h, w, 4))
-        return view.copy() if copy else view
+        """hg_readback_end_data: the image of the oldest begun readback, as (h, w, 4) float32 (RGBA32F), (h, w, 4)
+        float16 (RGBA16F) or (h, w) uint32 (R11G11B10F).  copy=False returns a view of the context's pinned host image,
+        valid until the depth-th readback_begin after the one it came from."""
+        ptr, n, fmt = C.c_void_p(), C.c_size_t(0), C.c_int32(-1)
+        self._check(lib().hg_readback_end_data(self._h, C.byref(ptr), C.byref(n), C.byref(fmt)), "hg_readback_end_data")
+        return _display_view(ptr, n.value, fmt.value, w, h, copy)
 
     def set_accumulation(self, image: np.ndarray, frame_count: int) -> None:
         """Checkpoint resume (hg_set_accumulation): the (h, w, 4) image hg_readback returned and the FrameCount of
@@ -376,6 +405,16 @@ class Comm:
                     "hg_comm_readback")
         return out
 
+    def readback_begin(self, fmt: int = HG_DISPLAY_RGBA32F) -> None:
+        """hg_comm_readback_begin: the pipelined display of the last gather's image (into the root context's ring)."""
+        self._check(lib().hg_comm_readback_begin(self._h, int(fmt)), "hg_comm_readback_begin")
+
+    def readback_end(self, w: int, h: int, copy: bool = True) -> np.ndarray:
+        """hg_comm_readback_end: the oldest begun display image (bounded wait), shaped as Context.readback_end's."""
+        ptr, n, fmt = C.c_void_p(), C.c_size_t(0), C.c_int32(-1)
+        self._check(lib().hg_comm_readback_end(self._h, C.byref(ptr), C.byref(n), C.byref(fmt)), "hg_comm_readback_end")
+        return _display_view(ptr, n.value, fmt.value, w, h, copy)
+
     def close(self):
         if getattr(self, "_h", None):
             lib().hg_comm_destroy(self._h)
@@ -406,6 +445,24 @@ def assemble_host(slabs: np.ndarray, width: int, height: int, n_ranks: int) -> n
                                      out.size)
     if rc != HG_OK:
         raise HalogenError(f"hg_comm_assemble_host failed ({rc}): slabs {s.shape} for {width}x{height}, {n_ranks} ranks")
+    return out
+
+
+def pack_display(rgba: np.ndarray, fmt: int) -> np.ndarray:
+    """hg_pack_display: (..., 4) float32 pixels in a display format on the host, the device's conversion (no GPU):
+    (..., 4) float32, (..., 4) float16 or (...) uint32 (R11G11B10F)."""
+    a = np.ascontiguousarray(rgba, dtype=np.float32)
+    if a.shape[-1] != 4:
+        raise ValueError("rgba must have 4 channels")
+    n = a.size // 4
+    shape = {HG_DISPLAY_RGBA32F: (a.shape, np.float32), HG_DISPLAY_RGBA16F: (a.shape, np.float16),
+             HG_DISPLAY_R11G11B10F: (a.shape[:-1], np.uint32)}
+    if fmt not in shape:
+        raise ValueError(f"unknown display format {fmt}")
+    out = np.empty(*shape[fmt])
+    rc = lib().hg_pack_display(a.ctypes.data_as(C.POINTER(C.c_float)), n, int(fmt), C.c_void_p(out.ctypes.data))
+    if rc != HG_OK:
+        raise HalogenError(f"hg_pack_display failed ({rc})")
     return out
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 3
+#define HG_ABI_VERSION 4
 
 /* ----------------------------------------------------------------------------------------------
  * Reference host structs (byte-identical to the C# [Sequential] structs)
@@ -217,8 +217,13 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   (each launches the held frames first).  The frames, their order and the image are those of separate launches; a
  *   launch has a fixed cost (its drain tail: ~0.35 ms on C3), so the reference's one call per frame (RP:327) runs at
  *   the multi-frame rate.  1 = every call launches at once. */
+/* HG_OPT_READBACK_DEPTH: display readbacks (hg_readback_begin[_format]) that may be outstanding at once, 1..8
+ *   (default 2: display one frame behind).  A deeper ring lets a caller that displays every frame keep more frames in
+ *   flight (display latency traded for throughput); changing it needs no readback outstanding. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9 };
+       HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
+       HG_OPT_READBACK_DEPTH = 10 };
+#define HG_READBACK_MAX 8
 
 int hg_abi_version(void);
 
@@ -264,15 +269,30 @@ int hg_synchronize(hg_ctx* ctx);
 int hg_readback(hg_ctx* ctx, float* rgba, size_t n_floats);
 
 /* Display readback, pipelined (the reference's per-frame Blit to rtCameraColor, RP:343-347, as a host image):
- * hg_readback_begin enqueues, after every frame rendered so far, the untiling of the accumulation target into a
- * row-major RGBA32F image and its copy into one of two pinned host images owned by the context, and returns at
- * once; hg_readback_end waits for the OLDEST begun readback and hands out its image (width*height*4 floats; with
- * tiling, other ranks' pixels are 0).  At most two readbacks are outstanding, so a caller can trace frame k+1 while
- * frame k's image crosses PCIe:  render(1); begin; if (2 outstanding) end -> display.
- * The pointer stays valid until the second hg_readback_begin after the one it came from, or until hg_resize /
- * hg_set_tiling / hg_destroy.  hg_readback_end launches no held frames (hg_readback_begin already did). */
+ * hg_readback_begin_format enqueues, after every frame rendered so far, the untiling of the accumulation target into a
+ * row-major image in a display format and its copy into the next of the context's pinned host images (a ring of
+ * HG_OPT_READBACK_DEPTH, default 2), and returns at once; hg_readback_end_data waits for the OLDEST begun readback and
+ * hands out its image (with tiling, other ranks' pixels are 0).  At most HG_OPT_READBACK_DEPTH readbacks are
+ * outstanding, so a caller can trace frame k+1 while frame k's image crosses PCIe:
+ *   render(1); begin; if (depth outstanding) end -> display        (one frame behind at depth 2)
+ * The pointer stays valid until the depth-th hg_readback_begin after the one it came from, or until hg_resize /
+ * hg_set_tiling / hg_destroy.  hg_readback_end launches no held frames (the begin already did).
+ * Formats (csrc/hg_pack.h has the exact conversion; the fp32 accumulation target is never changed):
+ *   HG_DISPLAY_RGBA32F     16 B/px, the accumulation target as it is;
+ *   HG_DISPLAY_RGBA16F      8 B/px, IEEE half per channel, round to nearest even, overflow to Inf, NaN -> 0x7E00;
+ *   HG_DISPLAY_R11G11B10F   4 B/px, DXGI_FORMAT_R11G11B10_FLOAT (R bits 0-10, G 11-21, B 22-31, no alpha): the URP
+ *                           HDR camera target the reference blits into (URP-HighFidelity.asset:26-27,
+ *                           m_HDRColorBufferPrecision 0); round to nearest even, overflow to +Inf, negatives and NaN
+ *                           to 0 (D3D's converter cannot run here: parity with it is unpinned).
+ * hg_readback_begin / hg_readback_end are the RGBA32F forms (hg_readback_end refuses a readback of another format). */
+enum { HG_DISPLAY_RGBA32F = 0, HG_DISPLAY_RGBA16F = 1, HG_DISPLAY_R11G11B10F = 2 };
+int hg_readback_begin_format(hg_ctx* ctx, int32_t format);
+int hg_readback_end_data(hg_ctx* ctx, const void** data, size_t* n_bytes, int32_t* format);
 int hg_readback_begin(hg_ctx* ctx);
 int hg_readback_end(hg_ctx* ctx, const float** rgba, size_t* n_floats);
+/* The display packing on the host (no device work): n_pixels RGBA32F pixels into `out` (16 / 8 / 4 B per pixel), the
+ * same conversion the device applies in hg_readback_begin_format. */
+int hg_pack_display(const float* rgba, size_t n_pixels, int32_t format, void* out);
 
 /* Checkpoint / resume: the inverse of hg_readback.  The reference's whole resumable state is the accumulation target
  * and FrameCount (RP:152, RP:185, RP:347).  Loads a row-major RGBA32F image (width*height*4 floats, as hg_readback
@@ -342,6 +362,12 @@ int hg_comm_synchronize(hg_comm* comm);
 /* On the process holding the root (after hg_comm_gather): the assembled image, width*height*4 floats. Blocks, with the
  * deadline of hg_comm_synchronize. */
 int hg_comm_readback(hg_comm* comm, float* rgba, size_t n_floats);
+/* Pipelined display of the gathered image (the multi-GPU form of hg_readback_begin_format / hg_readback_end_data; same
+ * formats): begin enqueues, after the last hg_comm_gather, the conversion of the root's assembled image and its copy
+ * into the root context's ring of pinned host images (that context's HG_OPT_READBACK_DEPTH) and returns at once; end
+ * waits for the oldest begun one with the deadline of hg_comm_synchronize and hands out its image. */
+int hg_comm_readback_begin(hg_comm* comm, int32_t format);
+int hg_comm_readback_end(hg_comm* comm, const void** data, size_t* n_bytes, int32_t* format);
 /* The deadline of every wait (default 120000 ms, or the environment variable HALOGEN_COMM_TIMEOUT_MS at init). */
 int hg_comm_set_timeout_ms(hg_comm* comm, int64_t timeout_ms);
 int hg_comm_transport(const hg_comm* comm);     /* HG_COMM_RCCL or HG_COMM_PEER */

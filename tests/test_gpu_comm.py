@@ -145,3 +145,44 @@ def test_gpu_comm_errors_are_loud(gpu):
         comm.close()
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["peer", "rccl"])
+def test_gpu_comm_display_readback_pipelined(gpu, transport):
+    """hg_comm_readback_begin / _end (the multi-GPU display path of the C# pass): the gathered image in every display
+    format, one and two frames behind, equals the host packing of the blocking fp32 readback of the same gather."""
+    packed, params, cube, _, acc = cases.setup("c1_64")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    n = 2 if transport == "peer" else 1
+    ctxs = [_rank_ctx(packed, params, cube, r, n, 0, abi.HG_KERNEL_AUTO) for r in range(n)]
+    comm = abi.Comm.all(ctxs) if transport == "peer" else abi.Comm.rank(ctxs[0], 1, abi.comm_unique_id(), 0)
+    try:
+        ctxs[0].set_option(abi.HG_OPT_READBACK_DEPTH, 3)
+        for fmt in (abi.HG_DISPLAY_R11G11B10F, abi.HG_DISPLAY_RGBA16F, abi.HG_DISPLAY_RGBA32F):
+            want, got = [], []
+            pending = 0
+            for _ in range(4):
+                for c in ctxs:
+                    c.render(1, acc)
+                comm.gather(0)
+                comm.readback_begin(fmt)
+                pending += 1
+                want.append(comm.readback(W, H))  # blocking fp32 readback of the same gather (waits for it)
+                if pending == 3:
+                    got.append(comm.readback_end(W, H))
+                    pending -= 1
+            while pending:
+                got.append(comm.readback_end(W, H))
+                pending -= 1
+            with pytest.raises(abi.HalogenError, match="no readback outstanding"):
+                comm.readback_end(W, H)
+            for k, (g, w) in enumerate(zip(got, want)):
+                h = abi.pack_display(w, fmt)
+                gb = g.view(np.uint32) if g.dtype == np.float32 else g.view(np.uint16) if g.dtype == np.float16 else g
+                hb = h.view(np.uint32) if h.dtype == np.float32 else h.view(np.uint16) if h.dtype == np.float16 else h
+                assert int((gb != hb).sum()) == 0, f"format {fmt}, frame {k + 1}"
+    finally:
+        comm.close()
+        for c in ctxs:
+            c.close()

@@ -8,7 +8,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu \
-    tests/test_gpu_per_frame.py tests/test_gpu_regen_noitems.py tests/test_gpu_check_exec.py \
+    tests/test_gpu_per_frame.py tests/test_gpu_display.py tests/test_gpu_regen_noitems.py tests/test_gpu_check_exec.py \
+    "tests/test_gpu_comm.py::test_gpu_comm_display_readback_pipelined" \
     "tests/test_gpu_parity.py::test_gpu_tile_order_bit_exact" > gpurun_out/pytest_a.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/pytest_a.log | tail -5
 ok $rc || exit $rc
