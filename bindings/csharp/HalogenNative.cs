@@ -69,7 +69,12 @@ public static class HalogenNative
     public const int HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
                      HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
-                     HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9;
+                     HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
+                     HG_OPT_READBACK_DEPTH = 10;
+    public const int HG_READBACK_MAX = 8;
+    // display formats of hg_readback_begin_format / hg_comm_readback_begin: 16 / 8 / 4 bytes per pixel; R11G11B10F is
+    // the URP HDR camera target the reference blits into (GraphicsFormat.B10G11R11_UFloatPack32: R in bits 0-10)
+    public const int HG_DISPLAY_RGBA32F = 0, HG_DISPLAY_RGBA16F = 1, HG_DISPLAY_R11G11B10F = 2;
     public const int HG_SELFTEST_RCP = 1, HG_SELFTEST_BUILD = 2, HG_BUILD_CHECK_EXEC = 1, HG_BUILD_NO_REGEN_ITEMS = 2;
     public const int HG_COMM_ID_BYTES = 128, HG_COMM_RCCL = 1, HG_COMM_PEER = 2;
 
@@ -92,6 +97,10 @@ public static class HalogenNative
     [DllImport(Lib)] public static extern int hg_readback(IntPtr ctx, float[] rgba, UIntPtr nFloats);
     [DllImport(Lib)] public static extern int hg_readback_begin(IntPtr ctx);
     [DllImport(Lib)] public static extern int hg_readback_end(IntPtr ctx, out IntPtr rgba, out UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_readback_begin_format(IntPtr ctx, int format);
+    [DllImport(Lib)] public static extern int hg_readback_end_data(IntPtr ctx, out IntPtr data, out UIntPtr nBytes,
+        out int format);
+    [DllImport(Lib)] public static extern int hg_pack_display(float[] rgba, UIntPtr nPixels, int format, IntPtr output);
     [DllImport(Lib)] public static extern int hg_set_accumulation(IntPtr ctx, float[] rgba, UIntPtr nFloats, int frameCount);
     [DllImport(Lib)] public static extern int hg_copy_tiles_device(IntPtr ctx, IntPtr dstDevice, UIntPtr nBytes);
     [DllImport(Lib)] public static extern int hg_local_tile_count(IntPtr ctx);
@@ -118,6 +127,9 @@ public static class HalogenNative
     [DllImport(Lib)] public static extern int hg_comm_gather(IntPtr comm, int root);
     [DllImport(Lib)] public static extern int hg_comm_synchronize(IntPtr comm);
     [DllImport(Lib)] public static extern int hg_comm_readback(IntPtr comm, float[] rgba, UIntPtr nFloats);
+    [DllImport(Lib)] public static extern int hg_comm_readback_begin(IntPtr comm, int format);
+    [DllImport(Lib)] public static extern int hg_comm_readback_end(IntPtr comm, out IntPtr data, out UIntPtr nBytes,
+        out int format);
     [DllImport(Lib)] public static extern int hg_comm_set_timeout_ms(IntPtr comm, long timeoutMs);
     [DllImport(Lib)] public static extern int hg_comm_transport(IntPtr comm);
     [DllImport(Lib)] public static extern IntPtr hg_comm_last_error(IntPtr comm);

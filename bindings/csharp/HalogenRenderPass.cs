@@ -14,6 +14,12 @@
 // the image's 8x8 tiles to them (hg_set_tiling) and gathers the accumulated tiles to device 0 once per displayed
 // frame over RCCL (hg_comm_init_all / hg_comm_gather); the image is identical to a one-GPU render.
 //
+// Display (RP:343-347): each frame's display readback is enqueued on the GPU (hg_readback_begin_format, or
+// hg_comm_readback_begin after the gather) and the image of HALOGEN_DISPLAY_LATENCY frames ago (default 1: one frame
+// behind) is shown, so the next frame traces while this one crosses PCIe.  The image comes in the format of the
+// reference's camera target, R11G11B10 float (URP-HighFidelity.asset:26-27, 4 B per pixel; HALOGEN_DISPLAY_FORMAT =
+// r11g11b10f | rgba16f | rgba32f), packed on the GPU; the fp32 accumulation target itself is never changed.
+//
 // No C# toolchain exists in the build image: this file is checked textually (public surface, the ABI calls it makes
 // exist in HalogenNative.cs and the header), not compiled.
 using System;
@@ -21,6 +27,7 @@ using System.Collections.Generic;
 using System.Runtime.InteropServices;
 using Unity.Mathematics;
 using UnityEngine;
+using UnityEngine.Experimental.Rendering;
 using UnityEngine.Rendering;
 using UnityEngine.Rendering.Universal;
 
@@ -91,9 +98,11 @@ public class HalogenRenderPass : ScriptableRenderPass
     int sceneSpheres, sceneMeshes;
 
     RTHandle rtDisplay;              // what the camera sees: the accumulated (or single) frame
-    Texture2D uploadTexture;         // RGBA32F staging for the read-back image
-    float[] pixels = Array.Empty<float>();
+    Texture2D uploadTexture;         // staging for the read-back image, in the display format
     bool haveImage;
+    readonly int displayFormat;      // HG_DISPLAY_* (HALOGEN_DISPLAY_FORMAT)
+    readonly int displayLatency;     // frames the shown image lags the traced one (HALOGEN_DISPLAY_LATENCY)
+    int displayPending;              // display readbacks enqueued and not yet shown
     readonly ProfilingSampler sampler = new ProfilingSampler("Halogen (MI355X)");
 
     // scene lists, rebuilt by UpdateObjectBuffers
@@ -118,6 +127,23 @@ public class HalogenRenderPass : ScriptableRenderPass
             int rc = HalogenNative.hg_create(d, out contexts[d]);
             if (rc != HalogenNative.HG_OK) throw new Exception($"hg_create({d}) failed ({rc}): no usable MI355X device");
         }
+
+        string fmt = (Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_FORMAT") ?? "r11g11b10f").ToLowerInvariant();
+        displayFormat = fmt == "rgba32f" ? HalogenNative.HG_DISPLAY_RGBA32F
+                      : fmt == "rgba16f" ? HalogenNative.HG_DISPLAY_RGBA16F : HalogenNative.HG_DISPLAY_R11G11B10F;
+        int latency = 1;
+        int.TryParse(Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_LATENCY") ?? "1", out latency);
+        displayLatency = Math.Min(Math.Max(latency, 0), HalogenNative.HG_READBACK_MAX - 1);
+        // the display ring lives on the context that displays (device 0; the gather's root)
+        Check(HalogenNative.hg_set_option(contexts[0], HalogenNative.HG_OPT_READBACK_DEPTH, displayLatency + 1),
+              "hg_set_option(HG_OPT_READBACK_DEPTH)");
+    }
+
+    GraphicsFormat DisplayGraphicsFormat()
+    {
+        if (displayFormat == HalogenNative.HG_DISPLAY_RGBA32F) return GraphicsFormat.R32G32B32A32_SFloat;
+        if (displayFormat == HalogenNative.HG_DISPLAY_RGBA16F) return GraphicsFormat.R16G16B16A16_SFloat;
+        return GraphicsFormat.B10G11R11_UFloatPack32;  // DXGI_FORMAT_R11G11B10_FLOAT: R in bits 0-10
     }
 
     ~HalogenRenderPass() { Dispose(); }
@@ -131,7 +157,7 @@ public class HalogenRenderPass : ScriptableRenderPass
         desc.enableRandomWrite = false;
         desc.bindMS = false;
         desc.depthBufferBits = 0;
-        desc.colorFormat = RenderTextureFormat.ARGBFloat;
+        desc.graphicsFormat = DisplayGraphicsFormat();
         RenderingUtils.ReAllocateIfNeeded(ref rtDisplay, desc, name: "_HalogenDisplay");
 
         var size = new Vector2Int(desc.width, desc.height);
@@ -148,9 +174,9 @@ public class HalogenRenderPass : ScriptableRenderPass
             Check(rc, "hg_comm_init_all");
         }
         if (uploadTexture != null) UnityEngine.Object.DestroyImmediate(uploadTexture);
-        uploadTexture = new Texture2D(size.x, size.y, TextureFormat.RGBAFloat, false, true);
-        pixels = new float[size.x * size.y * 4];
+        uploadTexture = new Texture2D(size.x, size.y, DisplayGraphicsFormat(), TextureCreationFlags.None);
         haveImage = false;
+        displayPending = 0;  // hg_resize / hg_set_tiling dropped the display readbacks in flight
         ClearAccumulation();
     }
 
@@ -230,26 +256,37 @@ public class HalogenRenderPass : ScriptableRenderPass
         }
         AccumulationBufferDirty = false;
 
-        var n = (UIntPtr)pixels.Length;
+        // the display image (RP:343-347), pipelined: enqueue this frame's readback on the GPU and show the one of
+        // `displayLatency` frames ago; with several GPUs the gather to device 0 comes first (bounded waits throughout)
+        int rc;
         if (comm != IntPtr.Zero)
         {
-            int rc = HalogenNative.hg_comm_gather(comm, 0);
-            if (rc == HalogenNative.HG_OK) rc = HalogenNative.hg_comm_readback(comm, pixels, n);
+            rc = HalogenNative.hg_comm_gather(comm, 0);
+            if (rc == HalogenNative.HG_OK) rc = HalogenNative.hg_comm_readback_begin(comm, displayFormat);
             if (rc != HalogenNative.HG_OK)
                 throw new Exception($"multi-GPU gather failed ({rc}): {Marshal.PtrToStringAnsi(HalogenNative.hg_comm_last_error(comm))}");
         }
         else
         {
-            // one GPU: untiled on the device and copied into the context's pinned image, loaded from there
-            Check(HalogenNative.hg_readback_begin(contexts[0]), "hg_readback_begin");
-            Check(HalogenNative.hg_readback_end(contexts[0], out IntPtr image, out UIntPtr nImage), "hg_readback_end");
-            uploadTexture.LoadRawTextureData(image, checked((int)nImage.ToUInt64() * sizeof(float)));
-            uploadTexture.Apply(false);
-            Graphics.Blit(uploadTexture, rtDisplay);
-            haveImage = true;
-            return;
+            Check(HalogenNative.hg_readback_begin_format(contexts[0], displayFormat), "hg_readback_begin_format");
         }
-        uploadTexture.SetPixelData(pixels, 0);
+        displayPending++;
+        if (displayPending <= displayLatency) return;  // the pipeline fills: keep showing the previous image
+        IntPtr image;
+        UIntPtr nBytes;
+        int format;
+        if (comm != IntPtr.Zero)
+        {
+            rc = HalogenNative.hg_comm_readback_end(comm, out image, out nBytes, out format);
+            if (rc != HalogenNative.HG_OK)
+                throw new Exception($"multi-GPU display failed ({rc}): {Marshal.PtrToStringAnsi(HalogenNative.hg_comm_last_error(comm))}");
+        }
+        else
+        {
+            Check(HalogenNative.hg_readback_end_data(contexts[0], out image, out nBytes, out format), "hg_readback_end_data");
+        }
+        displayPending--;
+        uploadTexture.LoadRawTextureData(image, checked((int)nBytes.ToUInt64()));
         uploadTexture.Apply(false);
         Graphics.Blit(uploadTexture, rtDisplay);
         haveImage = true;

@@ -9,6 +9,7 @@
 // (width, height, fov, position x y z, rotation x y z w, localToWorld 16 floats in Unity field order), frames, and optionally
 // cubemap PATH ("HGCUBE01", int32 face size, int32 mips, int64 float count, floats).  halogen/host_files.py writes
 // all three from the Python scene description.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -151,9 +152,48 @@ int main(int argc, char** argv) {
         std::printf("\n");
         return 0;
     }
+    if (mode == "display" && (argc == 6 || argc == 7)) {  // one Execute per frame with the pipelined display
+        const halogen::SceneBuffers scene = read_scene(argv[2]);
+        Config c = read_config(argv[3]);
+        halogen::Cubemap cube;
+        if (!c.cubemap_path.empty()) {
+            cube = read_cubemap(c.cubemap_path);
+            c.settings.environmentCubemap = &cube;
+        }
+        const std::string fmt_name = argv[5];
+        const int32_t fmt = fmt_name == "rgba32f" ? HG_DISPLAY_RGBA32F : fmt_name == "rgba16f" ? HG_DISPLAY_RGBA16F
+                            : fmt_name == "r11g11b10f" ? HG_DISPLAY_R11G11B10F : -1;
+        if (fmt < 0) die("display format must be rgba32f, rgba16f or r11g11b10f");
+        try {
+            halogen::HalogenRenderPass pass(c.settings, argc == 7 ? std::atoi(argv[6]) : 0);
+            pass.SetDisplay(fmt, 1);  // one frame behind, as the C# pass
+            int shown = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int32_t f = 0; f < c.frames; ++f) {
+                pass.Execute(scene, c.camera, 1);
+                if (pass.Display().data) ++shown;
+            }
+            const halogen::HalogenRenderPass::DisplayImage last = pass.FlushDisplay();
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (!last.data) die("no image displayed");
+            std::ofstream out(argv[4], std::ios::binary);
+            out.write(static_cast<const char*>(last.data), std::streamsize(last.bytes));
+            if (!out) die(std::string("cannot write ") + argv[4]);
+            std::printf("{\"frames\": %d, \"shown_while_rendering\": %d, \"frame_count\": %d, \"format\": %d, "
+                        "\"bytes\": %zu, \"ms_per_frame\": %.4f}\n",
+                        c.frames, shown, pass.getFrameCount(), last.format, last.bytes, ms / std::max(1, c.frames));
+        } catch (const halogen::HalogenError& e) {
+            std::fprintf(stderr, "halogen_render: %s\n", e.what());
+            return 1;
+        }
+        return 0;
+    }
     if (mode != "render" || argc < 5 || argc > 6) {
-        std::fprintf(stderr, "usage: %s render SCENE.hgscene CONFIG.txt OUT.f32 [device]\n       %s params CONFIG.txt\n",
-                     argv[0], argv[0]);
+        std::fprintf(stderr,
+                     "usage: %s render SCENE.hgscene CONFIG.txt OUT.f32 [device]\n"
+                     "       %s display SCENE.hgscene CONFIG.txt OUT.bin rgba32f|rgba16f|r11g11b10f [device]\n"
+                     "       %s params CONFIG.txt\n",
+                     argv[0], argv[0], argv[0]);
         return 2;
     }
     const halogen::SceneBuffers scene = read_scene(argv[2]);

@@ -185,6 +185,7 @@ class HalogenRenderPass {
     void OnCameraSetup(int32_t width, int32_t height) {
         if (width != prior_w_ || height != prior_h_) {
             check(hg_resize(ctx_, width, height), "hg_resize");
+            display_pending_ = 0;  // hg_resize drops the display readbacks in flight
             ClearAccumulation();
         }
         prior_w_ = width;
@@ -201,6 +202,7 @@ class HalogenRenderPass {
     // Multi-GPU (not in the reference): this pass renders only the 8x8 tiles t with t % n_ranks == rank
     void SetTiling(int32_t rank, int32_t n_ranks) {
         check(hg_set_tiling(ctx_, rank, n_ranks), "hg_set_tiling");
+        display_pending_ = 0;  // the new tiling drops the display readbacks in flight
         ClearAccumulation();
     }
 
@@ -246,7 +248,41 @@ class HalogenRenderPass {
         if (s_.Accumulate) FrameCount += n_frames;
     }
 
-    // The accumulated image, row-major RGBA32F (what the reference blits to the camera target)
+    // The reference's per-frame display (RP:343-347: the accumulation target blitted into the URP camera colour target,
+    // an R11G11B10 HDR target under URP-HighFidelity.asset:26-27) as a host image, pipelined: Display() enqueues the
+    // display readback of every frame rendered so far in the display format and returns the image of `latency` calls
+    // ago (an empty image while the pipeline fills), so the next Execute traces while that image crosses PCIe.
+    // FlushDisplay() waits for the readbacks in flight and returns the newest image.  The pointer stays valid until
+    // the next Display / FlushDisplay / OnCameraSetup with a new size.
+    struct DisplayImage {
+        const void* data = nullptr;
+        size_t bytes = 0;
+        int32_t format = HG_DISPLAY_R11G11B10F;
+    };
+    // format: HG_DISPLAY_R11G11B10F (the reference's camera target, 4 B/px), HG_DISPLAY_RGBA16F or HG_DISPLAY_RGBA32F;
+    // latency: 0 (each image before the next frame is traced) .. HG_READBACK_MAX - 1 frames behind
+    void SetDisplay(int32_t format, int32_t latency) {
+        if (latency < 0 || latency >= HG_READBACK_MAX) throw HalogenError("display latency out of range");
+        (void)FlushDisplay();
+        check(hg_set_option(ctx_, HG_OPT_READBACK_DEPTH, latency + 1), "hg_set_option(HG_OPT_READBACK_DEPTH)");
+        display_format_ = format;
+        display_latency_ = latency;
+    }
+    DisplayImage Display() {
+        check(hg_readback_begin_format(ctx_, display_format_), "hg_readback_begin_format");
+        ++display_pending_;
+        if (display_pending_ <= display_latency_) return DisplayImage{};
+        return end_display();
+    }
+    DisplayImage FlushDisplay() {
+        DisplayImage last{};
+        while (display_pending_ > 0) last = end_display();
+        return last;
+    }
+    int32_t display_format() const { return display_format_; }
+    int32_t display_latency() const { return display_latency_; }
+
+    // The accumulated image, row-major RGBA32F (what the reference blits to the camera target); blocks
     std::vector<float> Readback() {
         std::vector<float> img(size_t(prior_w_) * size_t(prior_h_) * 4);
         check(hg_readback(ctx_, img.data(), img.size()), "hg_readback");
@@ -286,6 +322,12 @@ class HalogenRenderPass {
     bool ObjectBuffersDirty = true;
 
    private:
+    DisplayImage end_display() {
+        DisplayImage d;
+        check(hg_readback_end_data(ctx_, &d.data, &d.bytes, &d.format), "hg_readback_end_data");
+        --display_pending_;
+        return d;
+    }
     void check(int rc, const char* what) const {
         if (rc != HG_OK) {
             const char* msg = ctx_ ? hg_last_error(ctx_) : nullptr;
@@ -296,6 +338,7 @@ class HalogenRenderPass {
     HalogenSettings settings_;
     ClampedSettings s_;
     hg_ctx* ctx_ = nullptr;
+    int32_t display_format_ = HG_DISPLAY_R11G11B10F, display_latency_ = 1, display_pending_ = 0;
     int32_t prior_w_ = -1, prior_h_ = -1;
     hg_vec3 prior_position_{};  // PriorCameraPosition / PriorCameraRotation (RP:293-294)
     hg_vec4 prior_rotation_{};

@@ -32,31 +32,34 @@ def test_gpu_display_format_equals_host_packing(gpu, fmt):
         ctx.set_params(params)
         ctx.render(1, True)
         ctx.readback_begin(fmt)
-        got = [ctx.readback_end(W, H)]
-        ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 4)  # three frames behind
+        got = [ctx.readback_end(W, H)]  # frame 1, at once
+        ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 4)  # up to four outstanding: three frames behind
         pending = 0
-        for _ in range(5):  # frames 2..6
+        for _ in range(5):  # frames 2..6; frames 2 and 3 are taken when the fourth readback is in flight
             ctx.render(1, True)
             ctx.readback_begin(fmt)
             pending += 1
             if pending == 4:
                 got.append(ctx.readback_end(W, H))
                 pending -= 1
+        ctx.readback_begin(fmt)  # frame 6 once more: four outstanding (frames 4, 5, 6, 6)
+        pending += 1
         with pytest.raises(abi.HalogenError, match="4 readbacks outstanding"):
             ctx.readback_begin(fmt)
         if fmt != abi.HG_DISPLAY_RGBA32F:
             with pytest.raises(abi.HalogenError, match="hg_readback_end_data"):  # the float-only entry point refuses
-                lib_ptr = abi.C.POINTER(abi.C.c_float)()
-                ctx._check(abi.lib().hg_readback_end(ctx._h, abi.C.byref(lib_ptr), None), "hg_readback_end")
+                ptr = abi.C.POINTER(abi.C.c_float)()
+                ctx._check(abi.lib().hg_readback_end(ctx._h, abi.C.byref(ptr), None), "hg_readback_end")
         while pending:
             got.append(ctx.readback_end(W, H))
             pending -= 1
-        assert len(got) == 6
-        for k, img in enumerate(got):
-            host = abi.pack_display(want[k], fmt)
+        frames_of = [1, 2, 3, 4, 5, 6, 6]
+        assert len(got) == len(frames_of)
+        for img, f in zip(got, frames_of):
+            host = abi.pack_display(want[f - 1], fmt)
             assert img.shape == host.shape and img.dtype == host.dtype
             bad = int((_bits(img) != _bits(host)).sum())
-            assert bad == 0, f"format {fmt}, frame {k + 1}: {bad} values differ from the host packing"
+            assert bad == 0, f"format {fmt}, frame {f}: {bad} values differ from the host packing"
         assert_bitwise(ctx.readback(W, H), want[-1], "accumulation target after the display readbacks")
 
 

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import cases
+from halogen import abi
 from halogen import host_files, render_pass as rp, scenes
 from halogen.unity import Transform
 
@@ -104,6 +105,34 @@ def test_gpu_cpp_render_pass_matches_golden(gpu, cli, tmp_path, name):
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), name
     for k in ("paths", "rays", "tri_tests", "aabb_tests"):
         assert cnt[k] == meta["counters"][k], (k, cnt[k], meta["counters"][k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["r11g11b10f", "rgba16f", "rgba32f"])
+@pytest.mark.parametrize("name", ["c1_64", "glass_64x36"])
+def test_gpu_cpp_pipelined_display_matches_golden(gpu, cli, tmp_path, name, fmt):
+    """The C++ pass's per-frame display (HalogenRenderPass::Display, one frame behind, as the C# pass): one Execute per
+    frame; the last displayed image is the golden image in the display format (hg_pack_display of the golden)."""
+    packed, settings, camera, frames, acc = cases.setup_host(name)
+    if not acc:
+        pytest.skip("accumulating cases only")
+    host_files.write_scene(packed, tmp_path / "s.hgscene")
+    cube = None
+    if settings.useHDRISky and settings.environmentCubemap is not None:
+        cube = tmp_path / "c.hgcube"
+        host_files.write_cubemap(settings.environmentCubemap, cube)
+    host_files.write_config(settings, camera, tmp_path / "s.cfg", frames=frames,
+                            cubemap_path=str(cube) if cube else None)
+    r = subprocess.run([str(cli), "display", str(tmp_path / "s.hgscene"), str(tmp_path / "s.cfg"),
+                        str(tmp_path / "img.bin"), fmt], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["frames"] == frames and out["shown_while_rendering"] == frames - 1
+    f = {"r11g11b10f": abi.HG_DISPLAY_R11G11B10F, "rgba16f": abi.HG_DISPLAY_RGBA16F, "rgba32f": abi.HG_DISPLAY_RGBA32F}[fmt]
+    want = abi.pack_display(np.load(GOLD / f"{name}.npz")["image"], f)
+    got = np.fromfile(tmp_path / "img.bin", dtype=np.uint8)
+    assert out["format"] == f and got.size == want.nbytes
+    assert np.array_equal(got, want.view(np.uint8).ravel()), (name, fmt)
 
 
 # ---- accumulation reset on camera change (RP:279-294): world position and rotation, Vector3/Quaternion.Equals ----
