@@ -48,6 +48,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 
 # VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per SIMD every 2 cycles
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles"), in G wave-instructions/s
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
+# Vector-memory data path (TD) floor: a wave-level load instruction holds a CU's texture-data unit for about 20 cycles
+# whatever its width (tools/micro_td_width.hip, tools/sweeps/micro_td_r03.json: 16-B loads, 4 lines per wave, 20.07
+# cycles, 30.6 G wave-loads/s on the GPU), so 256 CUs x 2.4 GHz / 20 cycles = 30.72 G wave-level VMEM instructions/s.
+# The traversal is bound by this unit (TD busy ~0.96), DESIGN.md sections 4.5, 10.
+VMEM_FLOOR_CYCLES = 20.0
+VMEM_PEAK_GINST = 256 * 2.4 / VMEM_FLOOR_CYCLES
 KERNEL_SYMBOL = {abi.HG_KERNEL_MEGA_POOL: "hg_trace_pool_kernel", abi.HG_KERNEL_MEGA_STREAM: "hg_trace_stream_kernel",
                  abi.HG_KERNEL_MEGA_REGEN: "hg_trace_regen_kernel", abi.HG_KERNEL_MEGA: "hg_trace_kernel",
                  abi.HG_KERNEL_WAVEFRONT: "hg_wf_trace"}
@@ -152,28 +158,44 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         ctx.render(1, True)
         ctx.readback(W, H, img)
     dt_rb = time.perf_counter() - t1
-    # display readback through the context's pinned images (hg_readback_begin/_end): the image of this frame before the
-    # next is traced (sync), or one frame behind so that frame k's copy overlaps frame k+1's trace (pipelined)
+    # display readback through the context's pinned images (hg_readback_begin_format / hg_readback_end_data), in each
+    # display format: the image of this frame before the next is traced (sync), one frame behind so that frame k's copy
+    # overlaps frame k+1's trace (pipelined: the C# / C++ passes' pattern), or three frames behind (depth 4)
     display = {}
-    for mode in ("sync", "pipelined"):
-        fresh()
-        ctx.synchronize()
-        t1 = time.perf_counter()
-        pending = 0
-        for _ in range(frames):
-            ctx.render(1, True)
-            ctx.readback_begin()
-            pending += 1
-            if mode == "sync" or pending == 2:
+    for fmt_name, fmt in abi.DISPLAY_FORMATS.items():
+        res = {"bytes_per_frame": W * H * abi.DISPLAY_BPP[fmt]}
+        for mode, depth in (("sync", 1), ("pipelined", 2), ("pipelined_depth4", 4)):
+            fresh()
+            ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+            ctx.synchronize()
+            t1 = time.perf_counter()
+            pending = 0
+            for _ in range(frames):
+                ctx.render(1, True)
+                ctx.readback_begin(fmt)
+                pending += 1
+                if pending == depth:
+                    ctx.readback_end(W, H, copy=False)
+                    pending -= 1
+            while pending:
                 ctx.readback_end(W, H, copy=False)
                 pending -= 1
-        while pending:
-            ctx.readback_end(W, H, copy=False)
-            pending -= 1
-        dt_d = time.perf_counter() - t1
-        display[mode] = {"value": paths / dt_d / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_d * 1e3 / frames}
+            dt_d = time.perf_counter() - t1
+            v = paths / dt_d / 1e6
+            res[mode] = {"value": v, "unit": "Mpaths/s", "ms_per_frame": dt_d * 1e3 / frames,
+                         "frac_of_batched": v / batched_value, "frames_behind": depth - 1}
+        display[fmt_name] = res
+    ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 2)
     last = ctx.readback(W, H)
     display["last_image_identical"] = bool(np.array_equal(batched.view(np.uint32), last.view(np.uint32)))
+    # the images of the last run (r11g11b10f, three frames behind) equal the host packing of the fp32 image
+    fresh()
+    for _ in range(frames):
+        ctx.render(1, True)
+    ctx.readback_begin(abi.HG_DISPLAY_R11G11B10F)
+    packed_img = ctx.readback_end(W, H)
+    display["r11g11b10f_equals_host_packing"] = bool(np.array_equal(
+        packed_img, abi.pack_display(ctx.readback(W, H), abi.HG_DISPLAY_R11G11B10F)))
     ctx.set_option(abi.HG_OPT_COALESCE, 32)
     value = paths * reps / dt / 1e6
     strict = paths * reps / dt_s / 1e6
@@ -186,6 +208,89 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
                               "readback_bytes_per_frame": W * H * 16},
             "with_display_readback": display,
             "bit_identical_to_batched": identical}
+
+
+def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dict:
+    """The reference's moving-camera frame (VERDICT r03 missing #3).  A camera move makes Execute call
+    ClearAccumulation, which sets ObjectBuffersDirty, so UpdateObjectBuffers gathers every scene array again and
+    SetBufferData re-uploads it before the dispatch (RP:262-268, 279-299, 448-509); the C# drop-in keeps that call
+    pattern (bindings/csharp/HalogenRenderPass.cs).  Per frame, as the drop-in issues it: hg_upload_scene (the same
+    arrays), hg_set_params with the moved camera (FrameCount 1), hg_clear_accumulation, hg_render(1) and the display
+    readback (R11G11B10F, one frame behind).  Reports ms per frame and the share spent inside hg_upload_scene (an
+    identical upload is detected and skipped by the library), and the cost of an upload whose arrays did change (a real
+    rebuild: validation, repack, copies), timed separately."""
+    import ctypes as C
+
+    from halogen.scene import PackedScene
+    from halogen.unity import Transform
+
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 2)
+    base = cfg.camera()
+    pos0 = tuple(base.transform.position)
+
+    def camera_at(k: int):
+        t = Transform((pos0[0] + 0.002 * k, pos0[1], pos0[2] - 0.001 * k), tuple(base.transform.rotation))
+        return rp.Camera(t, base.fieldOfView, W, H)
+
+    def frame_loop(n: int):
+        before = ctx.counters()
+        up = 0.0
+        pending = 0
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            tu = time.perf_counter()
+            ctx.upload_scene(packed)
+            up += time.perf_counter() - tu
+            ctx.set_params(rp.make_params(s, camera_at(k + 1), 1, len(packed.spheres), len(packed.meshes),
+                                          cube is not None))
+            ctx.clear_accumulation()
+            ctx.render(1, True)
+            ctx.readback_begin(abi.HG_DISPLAY_R11G11B10F)
+            pending += 1
+            if pending == 2:
+                ctx.readback_end(W, H, copy=False)
+                pending -= 1
+        while pending:
+            ctx.readback_end(W, H, copy=False)
+            pending -= 1
+        dt = time.perf_counter() - t0
+        after = ctx.counters()
+        return dt, up, after["scene_uploads_skipped"] - before["scene_uploads_skipped"], \
+            after["scene_uploads"] - before["scene_uploads"]
+
+    frame_loop(4)  # warm-up
+    dt, up, skipped, rebuilt = frame_loop(frames)
+
+    def copy(p):
+        arrays = {}
+        for k in ("spheres", "meshes", "materials", "triangles", "blas"):
+            a = getattr(p, k)
+            b = (type(a)._type_ * len(a))()
+            C.memmove(b, a, C.sizeof(a))
+            arrays[k] = b
+        return PackedScene(**arrays)
+
+    # a changed upload (one float of the last triangle moved, then moved back): every call rebuilds the device scene
+    alt = copy(packed)
+    alt.triangles[len(alt.triangles) - 1].pointA.x += 1e-3
+    rebuild = []
+    for k in range(4):
+        t0 = time.perf_counter()
+        ctx.upload_scene(alt if k % 2 == 0 else packed)
+        rebuild.append(time.perf_counter() - t0)
+    ctx.upload_scene(packed)
+    c = ctx.counters()
+    scene_bytes = sum(C.sizeof(getattr(packed, k)) for k in ("spheres", "meshes", "materials", "triangles", "blas"))
+    return {"workload": f"{frames} frames, camera moved before each: hg_upload_scene (same arrays) + hg_set_params + "
+                        f"hg_clear_accumulation + hg_render(1) + R11G11B10F display one frame behind (RP:262-299)",
+            "value": W * H * frames / dt / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt * 1e3 / frames,
+            "upload_ms_per_frame": up * 1e3 / frames, "upload_share": up / dt,
+            "uploads_skipped": skipped, "uploads_rebuilt": rebuilt, "scene_bytes": scene_bytes,
+            "changed_upload_ms": [x * 1e3 for x in rebuild],
+            "changed_upload_ms_mean": sum(rebuild) * 1e3 / len(rebuild),
+            "scene_uploads_total": c["scene_uploads"], "host_threads_upload": 16}
 
 
 def committed_counters(config: str, W: int, H: int, frames_per_launch: int, kernel_symbol: str) -> dict:
@@ -225,26 +330,46 @@ def launch_seconds(timing: dict) -> tuple:
 
 def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symbol: str, step_s: float = 0.0,
                 events_launch_s: float = 0.0) -> dict:
-    """The dominant kernel against what bounds it.  The trace kernel works on a cache-resident scene (C3: 90 MB,
-    inside the 256 MiB Infinity Cache) and is bound by VALU issue and latency, not HBM: `frac` is its VALU issue rate
-    (wave-level VALU instructions per launch, SQ_INSTS_VALU from the committed rocprofv3 pass of this workload and
-    build, over the launch time measured live with HIP events) against 1,024 SIMDs x 2.4 GHz / 2 cycles.
-    lane_util is the mean fraction of the 64 lanes active in those instructions, so frac x lane_util is the share of
-    the chip's fp32 lane-issue slots doing work.  HBM stays beside it: the PMC-measured DRAM-side bytes (traffic)
-    against 8 TB/s, and the §8(d) logical bytes.  vmem_unit_busy is the busy share of the vector-memory data path
-    (TD) from the same committed profile: the unit that binds the traversal, beside the VALU figure."""
+    """The dominant kernel against the unit that binds it.  The trace kernel works on a cache-resident scene (C3: 90 MB,
+    inside the 256 MiB Infinity Cache) and is bound by the vector-memory data path (the texture-data unit busy ~96 % of
+    the launch): `achieved` is its wave-level vector-memory instruction rate ((SQ_INSTS_VMEM_RD + SQ_INSTS_VMEM_WR) per
+    launch from the committed rocprofv3 pass of this workload and build, over the launch time measured live with HIP
+    events) against the per-CU instruction floor of that unit (VMEM_PEAK_GINST); td_busy / td_stalled_on_l1 sit beside
+    it.  The VALU issue rate is the secondary figure (`valu`: SQ_INSTS_VALU against 1,024 SIMDs x 2.4 GHz / 2 cycles).
+    HBM stays beside both: the PMC-measured DRAM-side bytes (traffic) against 8 TB/s, and the section 8(d) logical bytes."""
     ok = mean_launch_s > 0
     valu = pmc.get("valu_insts_per_launch")
-    achieved = valu / mean_launch_s / 1e9 if valu and ok else None
-    frac = achieved / VALU_PEAK_GINST if achieved else None
+    valu_achieved = valu / mean_launch_s / 1e9 if valu and ok else None
+    valu_frac = valu_achieved / VALU_PEAK_GINST if valu_achieved else None
     lane = pmc.get("valu_lane_util")
+    vmem = pmc.get("vmem_insts_per_launch")
+    vmem_achieved = vmem / mean_launch_s / 1e9 if vmem and ok else None
+    vmem_frac = vmem_achieved / VMEM_PEAK_GINST if vmem_achieved else None
+    busy = pmc.get("vmem_unit_busy") or {}
     traffic = pmc.get("hbm_bytes_per_launch")
     lib_sha = library_sha256()
-    return {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
-            "unit_note": "wave64 VALU instructions issued per second (peak = 1024 SIMDs x 2.4 GHz / 2 cycles)",
-            "frac": frac, "lane_util": lane, "useful_lane_frac": frac * lane if frac and lane else None,
-            "wait_any_frac": pmc.get("wait_any_frac"), "l2_hit_rate": pmc.get("l2_hit_rate"),
-            # the unit that binds (DESIGN §10): the texture-data path's busy share of the launch (PMC TD_TD_BUSY)
+    valu_obj = {"achieved": valu_achieved, "peak": VALU_PEAK_GINST, "unit": "Ginst/s", "frac": valu_frac,
+                "insts_per_launch": valu,
+                "unit_note": "wave64 VALU instructions issued per second (peak = 1024 SIMDs x 2.4 GHz / 2 cycles)",
+                "lane_util": lane, "useful_lane_frac": valu_frac * lane if valu_frac and lane else None,
+                "frac_per_launch_span": valu / events_launch_s / 1e9 / VALU_PEAK_GINST if valu and events_launch_s
+                else None,
+                "frac_per_step_period": valu / step_s / 1e9 / VALU_PEAK_GINST if valu and step_s else None}
+    vmem_obj = {"achieved": vmem_achieved, "peak": VMEM_PEAK_GINST, "unit": "Ginst/s", "frac": vmem_frac,
+                "insts_per_launch": vmem, "rd_per_launch": pmc.get("vmem_rd_insts_per_launch"),
+                "wr_per_launch": pmc.get("vmem_wr_insts_per_launch"),
+                "floor_cycles_per_inst": VMEM_FLOOR_CYCLES,
+                "unit_note": "wave-level vector-memory instructions per second against the texture-data unit's "
+                             "per-instruction floor (256 CUs x 2.4 GHz / 20 cycles, tools/micro_td_width.hip)",
+                "td_busy": busy.get("td_busy"), "td_stalled_on_l1": busy.get("td_stalled_on_l1"),
+                "ta_busy": busy.get("ta_busy"),
+                "frac_per_step_period": vmem / step_s / 1e9 / VMEM_PEAK_GINST if vmem and step_s else None}
+    bound_vmem = vmem_achieved is not None
+    top = vmem_obj if bound_vmem else valu_obj
+    return {"bound": "vmem" if bound_vmem else "valu", "achieved": top["achieved"], "peak": top["peak"],
+            "unit": top["unit"], "unit_note": top["unit_note"], "frac": top["frac"],
+            "vmem": vmem_obj, "valu": valu_obj,
+            "lane_util": lane, "wait_any_frac": pmc.get("wait_any_frac"), "l2_hit_rate": pmc.get("l2_hit_rate"),
             "vmem_unit_busy": pmc.get("vmem_unit_busy"),
             "traffic": traffic,
             "traffic_gbs": traffic / mean_launch_s / 1e9 if traffic and ok else None,
@@ -252,19 +377,17 @@ def roofline_of(pmc: dict, mean_launch_s: float, logical_per_launch, kernel_symb
             "hbm_peak_gbs": HBM_PEAK_GBS,
             "hbm_target_note": "north_star's >= 50 % of the HBM roofline during traversal does not apply: the scene "
                                "is cache-resident (L1/L2/Infinity Cache serve the BVH), so traffic_frac is the DRAM-side "
-                               "share, not a bound; the traversal is bound by the vector-memory data path "
-                               "(vmem_unit_busy.td_busy) and frac prices the VALU issue rate that follows from it "
-                               "(DESIGN.md sections 4.5, 10)",
+                               "share, not a bound; the traversal is bound by the vector-memory data path, whose "
+                               "instruction rate `frac` prices (DRAM-side traffic and VALU issue beside it; DESIGN.md "
+                               "sections 4.5, 10)",
             "write_bytes_per_launch": pmc.get("write_bytes_per_launch"),
             "logical_bytes_per_launch": logical_per_launch,
             "logical_gbs": logical_per_launch / mean_launch_s / 1e9 if logical_per_launch and ok else None,
             "mean_launch_ms": mean_launch_s * 1e3, "kernel": kernel_symbol,
             "launch_ms_basis": "union of the timed launches' HIP-event spans on both trace streams / launches",
             "mean_launch_span_ms": events_launch_s * 1e3 if events_launch_s else None,
-            "frac_per_launch_span": valu / events_launch_s / 1e9 / VALU_PEAK_GINST if valu and events_launch_s else None,
             # launches of consecutive steps overlap (two trace streams): the step period is the throughput's clock
             "step_period_ms": step_s * 1e3 if step_s else None,
-            "frac_per_step_period": valu / step_s / 1e9 / VALU_PEAK_GINST if valu and step_s else None,
             "counters_from": pmc.get("summary"),
             "counters_library_matches": (pmc.get("library_sha256") == lib_sha) if pmc.get("library_sha256") else None}
 
@@ -347,13 +470,14 @@ def main():
     ap.add_argument("--save-image", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + HALOGEN_BENCH_DEVICE=0: rehearse the N-rank path on one GPU (CPU collectives)")
-    ap.add_argument("--gather", default="torch", choices=["abi", "torch"],
-                    help="N > 1: the timed tile gather through torch.distributed (default: all_gather_into_tensor, then "
-                         "the C-ABI's host assembly) or through the C-ABI (hg_comm, RCCL send/recv + device assembly)")
+    ap.add_argument("--gather", default="abi", choices=["abi", "torch"],
+                    help="N > 1: the timed tile gather through the C-ABI (default: hg_comm, RCCL send/recv on the "
+                         "contexts' streams + device assembly, the drop-in's own path) or through torch.distributed "
+                         "(all_gather_into_tensor, assembled on rank 0's device through hg_comm_assemble_host's index)")
     ap.add_argument("--no-abi-check", action="store_true",
-                    help="N > 1 with nccl and the torch gather: skip the untimed hg_comm (RCCL) gather that is compared "
-                         "bit for bit with the timed gather (its failures are reported in the line, never hang: "
-                         "every hg_comm wait has a deadline)")
+                    help="N > 1: skip the untimed cross-check gather (the other transport of --gather), compared bit for "
+                         "bit with the timed gather and timed on its own (an hg_comm failure is reported in the line, "
+                         "never hangs: every hg_comm wait has a deadline)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
@@ -510,18 +634,49 @@ def main():
         gathered = gathered.cpu().numpy()
 
     abi_check = None
-    if dist is not None and comm is None and args.dist_backend == "nccl" and not args.no_abi_check:
-        # untimed: the C-ABI gather (RCCL send/recv + device assembly) of the same accumulators, bit for bit against the
-        # timed torch gather.  hg_comm waits are bounded, so a failure is reported here instead of hanging the ranks.
+    gather_ms = {}
+    if dist is not None and not args.no_abi_check:
+        import torch
+
+        from halogen import distributed as hd
+
+        def time_gather(fn):  # one gather alone, barrier + device sync on both sides, max over ranks (ms)
+            barrier()
+            t = time.perf_counter()
+            out = fn()
+            barrier()
+            v = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            return out, float(v.item()) * 1e3
+
+        def torch_gather():
+            loc = torch.empty((ctx.local_tile_count(), 64, 4), dtype=torch.float32, device=f"cuda:{device}")
+            ctx.copy_tiles_device(loc.data_ptr(), loc.numel() * 4)
+            return hd.gather_tiles(loc.to(coll_dev), rank, world, W, H, on_device=True)
+
+        def abi_gather(cm):
+            cm.gather(0)
+            cm.synchronize()
+            return None
+
+        # untimed cross-check: the other transport gathers the same accumulators; both gathers are also timed alone
         try:
-            with join_comm() as c2:
-                c2.gather(0)
-                c2.synchronize()
-                same = None
-                if rank == 0:
-                    img2 = c2.readback(W, H)
-                    same = bool(np.array_equal(img2.view(np.uint32), np.asarray(gathered).view(np.uint32)))
-                abi_check = {"ok": True, "transport": c2.transport, "bit_identical_to_timed_gather": same}
+            if comm is not None:  # timed: hg_comm; check: torch
+                _, gather_ms["abi"] = time_gather(lambda: abi_gather(comm))
+                timg, gather_ms["torch"] = time_gather(torch_gather)
+                same = bool(np.array_equal(timg.cpu().numpy().view(np.uint32), np.asarray(gathered).view(np.uint32))) \
+                    if rank == 0 else None
+                abi_check = {"ok": True, "checked_with": "torch all_gather_into_tensor", "bit_identical_to_timed_gather": same}
+            elif args.dist_backend == "nccl":  # timed: torch; check: hg_comm
+                _, gather_ms["torch"] = time_gather(torch_gather)
+                with join_comm() as c2:
+                    _, gather_ms["abi"] = time_gather(lambda: abi_gather(c2))
+                    same = None
+                    if rank == 0:
+                        img2 = c2.readback(W, H)
+                        same = bool(np.array_equal(img2.view(np.uint32), np.asarray(gathered).view(np.uint32)))
+                    abi_check = {"ok": True, "checked_with": f"hg_comm (transport {c2.transport})",
+                                 "bit_identical_to_timed_gather": same}
         except abi.HalogenError as e:
             abi_check = {"ok": False, "error": str(e)[:400]}
 
@@ -620,6 +775,8 @@ def main():
                                       "hg_comm_assemble_host's pixel index)"))
             if dist is not None else None,
             "abi_gather_check": abi_check,
+            # each gather alone (after the timed region; max over ranks): the one `gather` names is inside `value`
+            "gather_ms": gather_ms or None,
             "setup_s": setup_s,
             "kernel_ms": {"pipeline_total": cnt["kernel_ms"], "pipelines": cnt["launches"],
                           "trace_total": cnt["trace_ms"], "trace_busy": cnt.get("trace_busy_ms"),
@@ -633,6 +790,8 @@ def main():
         if world == 1 and not emu and not args.no_per_frame:
             result["per_frame"] = per_frame_measurement(ctx, params, W, H, frames_per_step, max(2, args.steps // 4),
                                                         result["value"])
+        if world == 1 and not emu and not args.no_per_frame:
+            result["camera_move"] = camera_move_measurement(ctx, packed, s, cfg, W, H, 32, cube)
         if world == 1 and not emu and args.config == "C3" and not args.no_counters and not args.no_framed:
             result["framed"] = framed_measurement(ctx, packed, s, W, H, frames_per_step, max(2, args.steps // 4))
         if world == 1 and not args.no_cpu_baseline:

@@ -63,6 +63,8 @@ public static class HalogenNative
         public ulong exec_fallbacks;
         public double trace_busy_ms;
         public ulong order_faults;
+        public ulong scene_uploads;
+        public ulong scene_uploads_skipped;
     }
 
     public const int HG_OK = 0;

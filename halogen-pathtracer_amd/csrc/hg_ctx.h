@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <string>
 #include <utility>
 #include <vector>
@@ -26,6 +27,10 @@ struct hg_ctx {
     int32_t n_spheres = 0, n_meshes = 0, n_materials = 0, n_tris = 0, n_nodes = 0;
     uint32_t stack_depth = 2;
     uint32_t hot_records = 0;  // HG_NODE_CACHE: device records [0, hot_records) are the BLAS tops (hot_prefix)
+    // the caller's arrays of the last upload (spheres, meshes, materials, triangles, BVH entries), byte for byte: an
+    // identical re-upload (the reference re-uploads on every camera move) is detected and skipped
+    std::vector<uint8_t> scene_copy[5];
+    uint64_t scene_uploads = 0, scene_uploads_skipped = 0;
 
     // cubemap
     DevBuf cube;

@@ -169,6 +169,10 @@ typedef struct hg_counters {
     uint64_t order_faults; /* HG_CHECK_EXEC builds only: cost-order sorts whose output was not a permutation of the tiles
                               (a placement out of range, or a tile placed other than once); must stay 0.  0 in product
                               builds */
+    uint64_t scene_uploads;         /* hg_upload_scene calls that (re)built the device scene, since hg_create */
+    uint64_t scene_uploads_skipped; /* ... and calls whose five arrays equalled the last upload's byte for byte, which
+                                       change nothing and return at once (the reference re-uploads on every camera
+                                       move: ClearAccumulation sets ObjectBuffersDirty, RP:262-268, 296-299) */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -233,7 +237,9 @@ void hg_destroy(hg_ctx* ctx);
 const char* hg_last_error(const hg_ctx* ctx);
 
 /* Upload the scene buffers (UpdateObjectBuffers, RP:448-509).  Validates every cross-reference
- * (offsets, child indices, material indices) before anything reaches the GPU. */
+ * (offsets, child indices, material indices) before anything reaches the GPU.  Arrays equal byte for byte to the last
+ * successful upload's are detected (a parallel compare against retained host copies) and change nothing: the call
+ * returns without touching the device (hg_counters.scene_uploads_skipped). */
 int hg_upload_scene(hg_ctx* ctx,
                     const HalogenSphere* spheres, int32_t n_spheres,
                     const HalogenMeshData* meshes, int32_t n_meshes,

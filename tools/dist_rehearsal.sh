@@ -7,7 +7,7 @@ export HALOGEN_BENCH_DEVICE=0
 ARGS="--config C3 --width 640 --height 360 --steps 1 --warmup 1 --no-cpu-baseline --frames-per-step 8"
 for n in 2 3; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-      --master-port $((29500 + n)) bench.py --gpus $n --dist-backend gloo $ARGS \
+      --master-port $((29500 + n)) bench.py --gpus $n --dist-backend gloo --gather torch --no-abi-check $ARGS \
       --save-image gpurun_out/dist/img_n$n.npy > gpurun_out/dist/bench_n$n.json 2> gpurun_out/dist/bench_n$n.err
   rc=$?; echo "n=$n rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dist/bench_n$n.err; exit $rc; }
   cat gpurun_out/dist/bench_n$n.json

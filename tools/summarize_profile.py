@@ -149,6 +149,11 @@ def main():
             t["valu_insts_per_launch"] = pmc["SQ_INSTS_VALU"]
             if pmc.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in pmc:
                 t["valu_lane_util"] = pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
+        if "SQ_INSTS_VMEM_RD" in pmc:
+            # wave-level vector-memory instructions per launch (bench.py roofline.vmem: against the TD unit's floor)
+            t["vmem_rd_insts_per_launch"] = pmc["SQ_INSTS_VMEM_RD"]
+            t["vmem_wr_insts_per_launch"] = pmc.get("SQ_INSTS_VMEM_WR")
+            t["vmem_insts_per_launch"] = pmc["SQ_INSTS_VMEM_RD"] + pmc.get("SQ_INSTS_VMEM_WR", 0.0)
         if "wave_cycle_split" in k:
             t["wait_any_frac"] = k["wave_cycle_split"].get("wait_any")
         if "l2_hit_rate" in k:
