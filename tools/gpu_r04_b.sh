@@ -3,6 +3,8 @@
 set -u
 mkdir -p gpurun_out
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+timeout -k 10 120 tools/micro_lane_order > gpurun_out/micro_lane_order.json; rc=$?
+echo "micro_lane_order rc=$rc"; cat gpurun_out/micro_lane_order.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu \
     tests/test_gpu_display.py "tests/test_gpu_comm.py::test_gpu_comm_display_readback_pipelined" \
     "tests/test_host_cpp.py::test_gpu_cpp_pipelined_display_matches_golden" tests/test_gpu_upload.py \
