@@ -170,11 +170,13 @@
 #define HG_COALESCE 32  // default HG_OPT_COALESCE: frames of consecutive hg_render calls held for one launch
 #endif
 #ifndef HG_TRACE_LANES
-#define HG_TRACE_LANES 8  // trace streams of the render pipeline (hg_ctx.h): chunks traced in turn on them, blended in
+#define HG_TRACE_LANES 12  // trace streams of the render pipeline (hg_ctx.h): chunks traced in turn on them, blended in
 #endif                    // order.  1-frame launches, C3, all waves per launch: 2 streams 1,970, 3: 2,143, 4: 2,265,
                           // 6: 2,242, 8: 2,302 Mpaths/s; with HG_QUEUE_WAVES_DIV 6 and 8 streams 2,745, with 8 and 10 / 12
                           // streams 2,808 / 2,790 (tools/sweeps/sweep_r03_u/v/y/z/aa; streams 3+ on hardware queues of
-                          // their own, HG_LANE_STREAMS)
+                          // their own, HG_LANE_STREAMS).  Round 4 (queue heads reset in-kernel, small sort), streams /
+                          // divisor 8/6 2,779-2,793, 12/8 2,874-2,878, 12/12 2,748-2,753, 16/12 2,893-2,908, 16/16
+                          // 2,800-2,808 (tools/sweeps/sweep_r04_a.txt): 12/8, +3 % for four more queues per context
 #ifndef HG_TRACE_LANES_BIG
 #define HG_TRACE_LANES_BIG 2  // of those, the ones chunks of more than HG_QUEUE_MAX_FRAMES frames take in turn (a third
 #endif                        // 64-frame launch beside two others: C3 -1.5 %)
@@ -188,8 +190,9 @@
 #define HG_LANE_STREAMS 3
 #endif
 #ifndef HG_QUEUE_WAVES_DIV
-#define HG_QUEUE_WAVES_DIV 6  // queue launches beside >= 2 other traces in flight: at most this many times fewer persistent
-#endif                        // waves than resident slots (hg_render; C3 1-frame launches, 8 streams: 1 2,265 -> 6 2,745)
+#define HG_QUEUE_WAVES_DIV 8  // queue launches beside >= 2 other traces in flight: at most this many times fewer persistent
+#endif                        // waves than resident slots (hg_render; C3 1-frame launches, 8 streams: 1 2,265 -> 6 2,745;
+                              // 12 streams: 8 2,874-2,878, 12 2,748-2,753)
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif

@@ -93,6 +93,7 @@ constexpr uint32_t kStreamLdsState = 10;
 // Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
 // 6-8, the distributed leaf test 10-12, the traversal stack from row 13.
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
+[[maybe_unused]] constexpr uint32_t kRowSort = 9;  // HG_RAY_SORT builds: the lane-permutation scratch row
 constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
 static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
 constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
@@ -843,6 +844,35 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
     y = ty * HG_TILE + ((slot >> 3) & 7u);
 }
 
+#ifndef HG_RAY_SORT
+#define HG_RAY_SORT 0  // A/B (DESIGN.md §10 lever 7): 1 = sort the lanes beginning a ray by direction octant, 2 = by
+                       // octant and dominant axis (24 keys), before their traversal
+#endif
+#if HG_RAY_SORT
+// Ray-coherence experiment.  A vector load costs the texture-data unit per distinct cache line in each 16-lane quarter
+// of the wave, not per line of the whole wave (tools/micro_lane_order.hip: 4 lines per instruction cost 19 cycles with
+// each line's lanes in one quarter and 51-65 with them spread), so rays that visit the same nodes should sit in the same
+// quarter.  The lanes that begin a ray in a shading pass (`began`) exchange their whole path state so that equal sort
+// keys are adjacent: a counting sort of the keys by ballots; lane l writes its own lane number to LDS word pos(l) of the
+// scratch row; the began lane of rank r among the began lanes reads word r, the lane whose state it takes; every state
+// word moves by ds_bpermute (full EXEC: the other lanes take their own).  Which lane runs a path changes no result.
+__device__ __forceinline__ uint32_t ray_key(const f3& d) {
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+#if HG_RAY_SORT == 2
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const uint32_t dom = ax >= ay && ax >= az ? 0u : ay >= az ? 1u : 2u;
+    return oct * 3u + dom;
+#else
+    return oct;
+#endif
+}
+constexpr uint32_t kRayKeys = HG_RAY_SORT == 2 ? 24u : 8u;
+__device__ __forceinline__ uint32_t bperm(uint32_t src, uint32_t v) {
+    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
+}
+__device__ __forceinline__ float bpermf(uint32_t src, float v) { return __uint_as_float(bperm(src, __float_as_uint(v))); }
+#endif
+
 // Streaming variant (HG_KERNEL_MEGA_STREAM): the regenerating kernel with a resumable traversal.  Lanes advance
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
 // some have finished), the finished lanes shade their hit and start their next ray while the stragglers keep
@@ -975,6 +1005,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         for (uint32_t it = 0;; ++it) {
             const uint32_t n_sh = wave_count(work && tv.mi >= nm);
             if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
+#if HG_RAY_SORT
+            bool began = false;  // this lane begins a ray (its traversal starts after the sort below)
+#endif
             if (work && tv.mi >= nm) {
             c.shade_rounds += wave_once();
 #if HG_PHASE_DETAIL == 1
@@ -1082,11 +1115,59 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 13, tp);
 #endif
+#if HG_RAY_SORT
+            began = alive;
+#else
             if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
+#endif
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 14, tp);
 #endif
             }
+#if HG_RAY_SORT
+            {  // converged: permute the began lanes' path states into key order, then begin their traversals
+                const uint64_t bm = wave_ballot(began);
+                if (__builtin_popcountll(bm) >= 2) {
+                    const uint32_t key = began ? ray_key(ray.d) : kRayKeys;
+                    uint32_t pos = 0, base = 0;
+                    for (uint32_t v = 0; v < kRayKeys; ++v) {
+                        const uint64_t m = wave_ballot(key == v);
+                        if (key == v)
+                            pos = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                        base += uint32_t(__builtin_popcountll(m));
+                    }
+                    uint32_t* const scratch = hg_lds_stack + kRowSort * 64u;
+                    if (began) scratch[pos] = lane;
+                    wave_lds_sync();
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
+                    const uint32_t src = began ? scratch[rank] : lane;
+                    wave_lds_sync();
+                    ray.o = mk(bpermf(src, ray.o.x), bpermf(src, ray.o.y), bpermf(src, ray.o.z));
+                    ray.d = mk(bpermf(src, ray.d.x), bpermf(src, ray.d.y), bpermf(src, ray.d.z));
+                    fs = bperm(src, fs);
+                    bounce = bperm(src, bounce);
+                    smp.frame = bperm(src, smp.frame);
+                    smp.pixel = bperm(src, smp.pixel);
+                    smp.offset = bperm(src, smp.offset);
+                    ms.s = (uint64_t(bperm(src, uint32_t(ms.s >> 32))) << 32) | bperm(src, uint32_t(ms.s));
+                    ms.sp = int(bperm(src, uint32_t(ms.sp)));
+                    acc_rough = bpermf(src, acc_rough);
+                    if constexpr (kQueue) slot = bperm(src, slot);
+                    else pix = bperm(src, pix);
+                    const RowVec3<kRowThr> o_thr{src};
+                    const RowVec3<kRowCol> o_col{src};
+                    const f3 t_thr = o_thr.get(), t_col = o_col.get();
+                    f3 t_sum = mk(0, 0, 0);
+                    if (kp.spp != 1) t_sum = RowVec3<kRowSum>{src}.get();
+                    wave_lds_sync();
+                    s_thr.set(t_thr);
+                    s_col.set(t_col);
+                    if (kp.spp != 1) s_sum.set(t_sum);
+                    wave_lds_sync();
+                }
+                if (began) trav_begin<kMeshLds>(kp, ray, tv, c);
+            }
+#endif
         }
 #if HG_SHADE_PRIO == 1
         __builtin_amdgcn_s_setprio(0);
