@@ -24,6 +24,7 @@
 #include "hg_tiling.h"
 #include "hg_interval.h"
 #include "hg_pack.h"
+#include "hg_host_pool.h"
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
@@ -256,25 +257,22 @@ uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32
     return hot;
 }
 
-// fn(begin, end) over [0, n) in contiguous chunks on up to `max_threads` threads (the caller's thread is one of them);
-// at least `grain` items per thread
+// fn(begin, end) over [0, n) in contiguous chunks on the persistent host pool (hg_host_pool.h), at most `max_threads`
+// chunks of at least `grain` items
 template <class F>
 void parallel_for(size_t n, size_t grain, int max_threads, F fn) {
-    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t t = std::max<size_t>(1, std::min<size_t>({size_t(max_threads), hw, (n + grain - 1) / std::max<size_t>(grain, 1)}));
+    HgHostPool& pool = HgHostPool::get();
+    const size_t t = std::max<size_t>(1, std::min<size_t>({size_t(max_threads), size_t(pool.threads()),
+                                                           (n + grain - 1) / std::max<size_t>(grain, 1)}));
     if (t <= 1) {
         fn(size_t(0), n);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(t - 1);
     const size_t chunk = (n + t - 1) / t;
-    for (size_t k = 1; k < t; ++k) {
+    pool.run(t, [&](size_t k) {
         const size_t b = std::min(n, k * chunk), e = std::min(n, b + chunk);
-        if (b < e) th.emplace_back([&fn, b, e] { fn(b, e); });
-    }
-    fn(size_t(0), std::min(n, chunk));
-    for (auto& x : th) x.join();
+        if (b < e) fn(b, e);
+    });
 }
 
 // Byte equality of two buffers, compared in parallel chunks (the scene's triangle array is 63 MB at C3)
@@ -612,7 +610,8 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if (c->has_scene) {
         bool same = true;
         for (int k = 0; k < 5 && same; ++k) same = c->scene_copy[k].size() == bytes_in[k];
-        for (int k = 0; k < 5 && same; ++k) same = same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]);
+        for (int k = 0; k < 3 && same; ++k) same = !bytes_in[k] || !std::memcmp(c->scene_copy[k].data(), src[k], bytes_in[k]);
+        for (int k = 3; k < 5 && same; ++k) same = same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]);
         if (same) {
             c->scene_uploads_skipped++;
             return HG_OK;

@@ -67,3 +67,32 @@ def test_oracle_bvh_builder_under_asan_ubsan(asan):
 def test_parallel_blas_builder_under_tsan(tsan):
     out = run([tsan, 40000, 7, 2, 5, 16])
     assert out.count("identical") == 3
+
+
+POOL_DRIVER = r'''
+#include "hg_host_pool.h"
+#include <cstdio>
+#include <vector>
+int main() {
+    std::vector<long> v(1000, 0);
+    for (int rep = 0; rep < 500; ++rep)  // many back-to-back jobs: the generation / done hand-off between jobs
+        HgHostPool::get().run(37, [&](size_t t) { for (size_t i = t; i < v.size(); i += 37) v[i] += 1; });
+    long s = 0;
+    for (long x : v) s += x;
+    std::printf("%ld %d\n", s, HgHostPool::get().threads());
+    return s == 500L * 1000 ? 0 : 1;
+}
+'''
+
+
+def test_host_pool_under_tsan(tmp_path):
+    """The persistent host pool of hg_upload_scene (csrc/hg_host_pool.h) under ThreadSanitizer: every task of every
+    job runs exactly once, with no data race between jobs."""
+    (tmp_path / "pool.cpp").write_text(POOL_DRIVER)
+    exe = tmp_path / "pool"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread",
+                    f"-I{ROOT / 'halogen-pathtracer_amd' / 'csrc'}", str(tmp_path / "pool.cpp"), "-o", str(exe),
+                    "-lpthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-2000:]
+    assert r.stdout.split()[0] == str(500 * 1000)
