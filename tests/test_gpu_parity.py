@@ -47,6 +47,8 @@ def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=Non
     if os.environ.get("HG_EXPECT_NO_EXEC_FALLBACK") == "1":  # tests/test_gpu_check_exec.py: an HG_CHECK_EXEC=1 build
         assert ctx.selftest(abi.HG_SELFTEST_BUILD)[0] & abi.HG_BUILD_CHECK_EXEC, f"{abi.LIB_PATH} is not a check build"
         assert cnt["exec_fallbacks"] == 0, f"leaf_dist ran under a partial EXEC {cnt['exec_fallbacks']} times"
+        # the cost order of every sort was a permutation of the tiles (hg_order_verify)
+        assert cnt["order_faults"] == 0, f"{cnt['order_faults']} cost-order placements out of range or repeated"
     if own:
         ctx.close()
     return img, cnt
