@@ -164,9 +164,12 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     display = {}
     for fmt_name, fmt in abi.DISPLAY_FORMATS.items():
         res = {"bytes_per_frame": W * H * abi.DISPLAY_BPP[fmt]}
-        for mode, depth in (("sync", 1), ("pipelined", 2), ("pipelined_depth4", 4)):
+        for mode, depth, side in (("sync", 1, 0), ("pipelined", 2, 0), ("pipelined_depth4", 4, 0),
+                                  ("pipelined_side", 2, 1), ("pipelined_depth4_side", 4, 1),
+                                  ("pipelined_depth8_side", 8, 1)):
             fresh()
             ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+            ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)
             ctx.synchronize()
             t1 = time.perf_counter()
             pending = 0
@@ -183,9 +186,11 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
             dt_d = time.perf_counter() - t1
             v = paths / dt_d / 1e6
             res[mode] = {"value": v, "unit": "Mpaths/s", "ms_per_frame": dt_d * 1e3 / frames,
-                         "frac_of_batched": v / batched_value, "frames_behind": depth - 1}
+                         "frac_of_batched": v / batched_value, "frames_behind": depth - 1,
+                         "copy_stream": "side" if side else "context"}
         display[fmt_name] = res
     ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 2)
+    ctx.set_option(abi.HG_OPT_READBACK_STREAM, 0)
     last = ctx.readback(W, H)
     display["last_image_identical"] = bool(np.array_equal(batched.view(np.uint32), last.view(np.uint32)))
     # the images of the last run (r11g11b10f, three frames behind) equal the host packing of the fp32 image

@@ -108,6 +108,10 @@ struct hg_ctx {
     int32_t image_host_format[HG_READBACK_MAX] = {};
     hipEvent_t image_copied[HG_READBACK_MAX] = {};
     int rb_depth = 2;                 // HG_OPT_READBACK_DEPTH: readbacks that may be outstanding
+    int rb_side = HG_READBACK_SIDE;   // HG_OPT_READBACK_STREAM: copies on rb_stream from per-slot device images
+    hipStream_t rb_stream = nullptr;
+    DevBuf rb_image[HG_READBACK_MAX];
+    hipEvent_t rb_untiled[HG_READBACK_MAX] = {};
     int rb_next = 0, rb_pending = 0;  // host image the next begin fills; begun readbacks not yet ended (<= rb_depth)
 };
 

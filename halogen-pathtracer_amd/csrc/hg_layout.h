@@ -193,6 +193,9 @@
 #define HG_QUEUE_WAVES_DIV 8  // queue launches beside >= 2 other traces in flight: at most this many times fewer persistent
 #endif                        // waves than resident slots (hg_render; C3 1-frame launches, 8 streams: 1 2,265 -> 6 2,745;
                               // 12 streams: 8 2,874-2,878, 12 2,748-2,753)
+#ifndef HG_READBACK_SIDE
+#define HG_READBACK_SIDE 0  // default HG_OPT_READBACK_STREAM (display copies on a side stream)
+#endif
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif

@@ -351,6 +351,7 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
 // trace in flight may read are changed or freed)
 int quiesce(hg_ctx* c) {
     HG_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->rb_stream) HG_HIP(c, hipStreamSynchronize(c->rb_stream));
     for (hg_ctx::TraceLane& L : c->lanes)
         if (L.stream) HG_HIP(c, hipStreamSynchronize(L.stream));
     return HG_OK;
@@ -567,11 +568,15 @@ void hg_destroy(hg_ctx* c) {
         if (L.blended) (void)hipEventDestroy(L.blended);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
+    if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
     release(c->image);
     for (int k = 0; k < HG_READBACK_MAX; ++k) {
+        release(c->rb_image[k]);
+        if (c->rb_untiled[k]) (void)hipEventDestroy(c->rb_untiled[k]);
         if (c->image_host[k]) (void)hipHostFree(c->image_host[k]);
         if (c->image_copied[k]) (void)hipEventDestroy(c->image_copied[k]);
     }
+    if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
     if (c->poll_host) (void)hipHostFree(c->poll_host);
     for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
     for (auto& pr : c->pending_trace) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1256,31 +1261,33 @@ size_t display_bpp(int32_t format) {
 }
 
 template <bool kRows>
-void launch_untile(hg_ctx* c, int32_t format, const float4* src) {
+void launch_untile(hg_ctx* c, void* dst, int32_t format, const float4* src) {
     const size_t pixels = size_t(c->W) * size_t(c->H);
     const dim3 g(uint32_t((pixels + 255) / 256)), b(256);
     if (format == HG_DISPLAY_RGBA16F)
-        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA16F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
-                           c->H, c->tiles_x, c->rank, c->n_ranks);
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA16F, kRows>), g, b, 0, c->stream, dst, src, c->W, c->H,
+                           c->tiles_x, c->rank, c->n_ranks);
     else if (format == HG_DISPLAY_R11G11B10F)
-        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_R11G11B10F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
-                           c->H, c->tiles_x, c->rank, c->n_ranks);
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_R11G11B10F, kRows>), g, b, 0, c->stream, dst, src, c->W, c->H,
+                           c->tiles_x, c->rank, c->n_ranks);
     else
-        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA32F, kRows>), g, b, 0, c->stream, c->image.p, src, c->W,
-                           c->H, c->tiles_x, c->rank, c->n_ranks);
+        hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA32F, kRows>), g, b, 0, c->stream, dst, src, c->W, c->H,
+                           c->tiles_x, c->rank, c->n_ranks);
 }
 
 // Enqueue on the context stream: the accumulator untiled (or, with `rows`, a row-major float4 image of the target's
-// size converted) into c->image (grown as needed) in `format`.  Returns its size in bytes.
-int untile_async(hg_ctx* c, size_t* bytes, int32_t format = HG_DISPLAY_RGBA32F, const float4* rows = nullptr) {
+// size converted) into `target` (c->image unless given; grown as needed) in `format`.  Returns its size in bytes.
+int untile_async(hg_ctx* c, size_t* bytes, int32_t format = HG_DISPLAY_RGBA32F, const float4* rows = nullptr,
+                 DevBuf* target = nullptr) {
+    DevBuf& img = target ? *target : c->image;
     const size_t pixels = size_t(c->W) * size_t(c->H);
     *bytes = pixels * display_bpp(format);
-    if (c->image.bytes < *bytes) {  // everything that might read the old image is ordered before on the context stream
+    if (img.bytes < *bytes) {  // everything that might read the old image is ordered before on the context stream
         HG_HIP(c, hipStreamSynchronize(c->stream));
-        if (int rc = ensure(c, c->image, *bytes)) return rc;
+        if (int rc = ensure(c, img, *bytes)) return rc;
     }
-    if (rows) launch_untile<true>(c, format, rows);
-    else launch_untile<false>(c, format, static_cast<const float4*>(c->acc.p));
+    if (rows) launch_untile<true>(c, img.p, format, rows);
+    else launch_untile<false>(c, img.p, format, static_cast<const float4*>(c->acc.p));
     HG_HIP(c, hipGetLastError());
     return HG_OK;
 }
@@ -1297,9 +1304,18 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
         return fail(c, HG_E_INVALID, "%d readbacks outstanding (HG_OPT_READBACK_DEPTH): call hg_readback_end first",
                     c->rb_pending);
     if (int rc = set_device(c)) return rc;
-    size_t bytes = 0;
-    if (int rc = untile_async(c, &bytes, format, static_cast<const float4*>(rows))) return rc;
     const int k = c->rb_next;  // not outstanding: at most rb_depth are, and k is the slot after the newest
+    // HG_OPT_READBACK_STREAM: the slot's own device image, copied on the side stream, so the context stream (the next
+    // frames' blends) does not wait for the copy; else c->image, copied on the context stream
+    const bool side = c->rb_side != 0;
+    if (side && !c->rb_stream) {
+        HG_HIP(c, hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking));
+        for (int j = 0; j < HG_READBACK_MAX; ++j)
+            HG_HIP(c, hipEventCreateWithFlags(&c->rb_untiled[j], hipEventDisableTiming));
+    }
+    size_t bytes = 0;
+    DevBuf* dimg = side ? &c->rb_image[k] : &c->image;
+    if (int rc = untile_async(c, &bytes, format, static_cast<const float4*>(rows), dimg)) return rc;
     if (c->image_host_cap[k] < bytes) {
         if (c->image_host[k]) {
             HG_HIP(c, hipEventSynchronize(c->image_copied[k]));  // (its last copy was ended, so this returns at once)
@@ -1312,8 +1328,15 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
         c->image_host_cap[k] = bytes;
         if (!c->image_copied[k]) HG_HIP(c, hipEventCreateWithFlags(&c->image_copied[k], hipEventDisableTiming));
     }
-    HG_HIP(c, hipMemcpyAsync(c->image_host[k], c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HG_HIP(c, hipEventRecord(c->image_copied[k], c->stream));
+    if (side) {
+        HG_HIP(c, hipEventRecord(c->rb_untiled[k], c->stream));
+        HG_HIP(c, hipStreamWaitEvent(c->rb_stream, c->rb_untiled[k], 0));
+        HG_HIP(c, hipMemcpyAsync(c->image_host[k], dimg->p, bytes, hipMemcpyDeviceToHost, c->rb_stream));
+        HG_HIP(c, hipEventRecord(c->image_copied[k], c->rb_stream));
+    } else {
+        HG_HIP(c, hipMemcpyAsync(c->image_host[k], dimg->p, bytes, hipMemcpyDeviceToHost, c->stream));
+        HG_HIP(c, hipEventRecord(c->image_copied[k], c->stream));
+    }
     c->image_host_bytes[k] = bytes;
     c->image_host_format[k] = format;
     c->rb_next = (k + 1) % c->rb_depth;
@@ -1577,6 +1600,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             if (c->rb_pending) return fail(c, HG_E_INVALID, "readbacks outstanding: end them before changing the depth");
             c->rb_depth = value;
             c->rb_next = 0;
+            return HG_OK;
+        case HG_OPT_READBACK_STREAM:
+            if (c->rb_pending) return fail(c, HG_E_INVALID, "readbacks outstanding: end them before changing the stream");
+            c->rb_side = value ? 1 : 0;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");

@@ -226,7 +226,10 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   flight (display latency traded for throughput); changing it needs no readback outstanding. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
-       HG_OPT_READBACK_DEPTH = 10 };
+       HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11 };
+/* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
+ *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
+ *   device image and copied on the context stream.  Same images either way. */
 #define HG_READBACK_MAX 8
 
 int hg_abi_version(void);

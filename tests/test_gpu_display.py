@@ -19,8 +19,9 @@ def _bits(a):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("side", [0, 1])
 @pytest.mark.parametrize("fmt", FORMATS)
-def test_gpu_display_format_equals_host_packing(gpu, fmt):
+def test_gpu_display_format_equals_host_packing(gpu, fmt, side):
     packed, params, cube, frames, acc = cases.setup("glass_64x36")  # emissive + sky: values above 1 and tiny ones
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)
     want = [gpu_render(packed, params, k, True, cube)[0] for k in (1, 2, 3, 4, 5, 6)]
@@ -30,6 +31,7 @@ def test_gpu_display_format_equals_host_packing(gpu, fmt):
             ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
         ctx.resize(W, H)
         ctx.set_params(params)
+        ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)  # copies on the context stream or on the side stream
         ctx.render(1, True)
         ctx.readback_begin(fmt)
         got = [ctx.readback_end(W, H)]  # frame 1, at once
