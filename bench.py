@@ -465,6 +465,10 @@ def main():
     ap.add_argument("--display", choices=["none", "sync", "pipelined"], default="none",
                     help="--per-frame-only: the display readback (hg_readback_begin/_end) after every call, as the "
                          "per_frame leg's with_display_readback")
+    ap.add_argument("--display-format", default="rgba32f", choices=sorted(abi.DISPLAY_FORMATS),
+                    help="--per-frame-only with --display: the display format")
+    ap.add_argument("--readback-depth", type=int, default=2, help="--per-frame-only, --display pipelined: readbacks "
+                    "in flight (HG_OPT_READBACK_DEPTH)")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
     ap.add_argument("--frames-per-step", type=int, default=64,
@@ -566,6 +570,9 @@ def main():
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
     if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step of the same launches, then steps x frames x hg_render(1)
         ctx.set_option(abi.HG_OPT_COALESCE, args.coalesce)
+        depth = 1 if args.display == "sync" else args.readback_depth
+        ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+        fmt = abi.DISPLAY_FORMATS[args.display_format]
         for _ in range(frames_per_step // args.launch_frames):  # warm-up step of the timed launches (their buffers)
             ctx.render(args.launch_frames, True)
         ctx.clear_accumulation()
@@ -577,9 +584,9 @@ def main():
         for _ in range(args.steps * frames_per_step // args.launch_frames):
             ctx.render(args.launch_frames, True)
             if args.display != "none":
-                ctx.readback_begin()
+                ctx.readback_begin(fmt)
                 pending += 1
-                if args.display == "sync" or pending == 2:
+                if pending == depth:
                     ctx.readback_end(W, H, copy=False)
                     pending -= 1
         while pending:

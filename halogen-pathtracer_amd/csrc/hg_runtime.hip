@@ -1229,9 +1229,9 @@ int hg_ctx_flush(hg_ctx* c) {
 
 // The accumulator (this rank's tiles, tile-major) as a row-major image in a display format (hg_pack.h); pixels of
 // other ranks' tiles are 0.  One thread per pixel: the stores are contiguous (16 / 8 / 4 B per pixel), the loads are 8
-// consecutive float4 per tile row.
+// consecutive float4 per tile row.  64-thread workgroups (see launch_untile).
 template <int kFmt, bool kRows>
-__global__ __launch_bounds__(256) void hg_untile_image(void* __restrict__ image, const float4* __restrict__ acc,
+__global__ __launch_bounds__(64) void hg_untile_image(void* __restrict__ image, const float4* __restrict__ acc,
                                                        int32_t W, int32_t H, int32_t tiles_x, int32_t rank,
                                                        int32_t n_ranks) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1262,8 +1262,10 @@ size_t display_bpp(int32_t format) {
 
 template <bool kRows>
 void launch_untile(hg_ctx* c, void* dst, int32_t format, const float4* src) {
+    // one-wave workgroups with few registers: a display readback's untile runs beside the persistent trace waves of the
+    // next frames (which hold most wave slots), as the lean blend does, instead of waiting for a CU to drain
     const size_t pixels = size_t(c->W) * size_t(c->H);
-    const dim3 g(uint32_t((pixels + 255) / 256)), b(256);
+    const dim3 g(uint32_t((pixels + 63) / 64)), b(64);
     if (format == HG_DISPLAY_RGBA16F)
         hipLaunchKernelGGL((hg_untile_image<HG_DISPLAY_RGBA16F, kRows>), g, b, 0, c->stream, dst, src, c->W, c->H,
                            c->tiles_x, c->rank, c->n_ranks);
