@@ -285,6 +285,14 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
         t0 = time.perf_counter()
         ctx.upload_scene(alt if k % 2 == 0 else packed)
         rebuild.append(time.perf_counter() - t0)
+    # an object moved (the last mesh translated, then back): triangles and BVH as before, a partial re-upload
+    moved = copy(packed)
+    moved.meshes[len(moved.meshes) - 1].worldToLocal.m[12] += 0.05
+    partial = []
+    for k in range(4):
+        t0 = time.perf_counter()
+        ctx.upload_scene(moved if k % 2 == 0 else packed)
+        partial.append(time.perf_counter() - t0)
     ctx.upload_scene(packed)
     c = ctx.counters()
     scene_bytes = sum(C.sizeof(getattr(packed, k)) for k in ("spheres", "meshes", "materials", "triangles", "blas"))
@@ -295,6 +303,9 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
             "uploads_skipped": skipped, "uploads_rebuilt": rebuilt, "scene_bytes": scene_bytes,
             "changed_upload_ms": [x * 1e3 for x in rebuild],
             "changed_upload_ms_mean": sum(rebuild) * 1e3 / len(rebuild),
+            "object_moved_upload_ms": [x * 1e3 for x in partial],
+            "object_moved_upload_ms_mean": sum(partial) * 1e3 / len(partial),
+            "scene_uploads_partial": c["scene_uploads_partial"],
             "scene_uploads_total": c["scene_uploads"], "host_threads_upload": 16}
 
 

@@ -65,6 +65,7 @@ public static class HalogenNative
         public ulong order_faults;
         public ulong scene_uploads;
         public ulong scene_uploads_skipped;
+        public ulong scene_uploads_partial;
     }
 
     public const int HG_OK = 0;

@@ -30,7 +30,8 @@ struct hg_ctx {
     // the caller's arrays of the last upload (spheres, meshes, materials, triangles, BVH entries), byte for byte: an
     // identical re-upload (the reference re-uploads on every camera move) is detected and skipped
     std::vector<uint8_t> scene_copy[5];
-    uint64_t scene_uploads = 0, scene_uploads_skipped = 0;
+    std::vector<HgDevMesh> dev_meshes;  // the device mesh table of the last upload (partial re-uploads start from it)
+    uint64_t scene_uploads = 0, scene_uploads_skipped = 0, scene_uploads_partial = 0;
 
     // cubemap
     DevBuf cube;

@@ -612,21 +612,17 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     const size_t bytes_in[5] = {size_t(n_spheres) * sizeof(HalogenSphere), size_t(n_meshes) * sizeof(HalogenMeshData),
                                 size_t(n_materials) * sizeof(PackedHalogenMaterial),
                                 size_t(n_tris) * sizeof(HalogenTriangle), size_t(n_nodes) * sizeof(BVHEntry)};
+    bool same[5] = {false, false, false, false, false};
     if (c->has_scene) {
-        bool same = true;
-        for (int k = 0; k < 5 && same; ++k) same = c->scene_copy[k].size() == bytes_in[k];
-        for (int k = 0; k < 3 && same; ++k) same = !bytes_in[k] || !std::memcmp(c->scene_copy[k].data(), src[k], bytes_in[k]);
-        for (int k = 3; k < 5 && same; ++k) same = same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]);
-        if (same) {
+        for (int k = 0; k < 5; ++k) same[k] = c->scene_copy[k].size() == bytes_in[k];
+        for (int k = 0; k < 3; ++k)
+            same[k] = same[k] && (!bytes_in[k] || !std::memcmp(c->scene_copy[k].data(), src[k], bytes_in[k]));
+        for (int k = 3; k < 5; ++k) same[k] = same[k] && same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]);
+        if (same[0] && same[1] && same[2] && same[3] && same[4]) {
             c->scene_uploads_skipped++;
             return HG_OK;
         }
     }
-    if (int rc = set_device(c)) return rc;
-    if (int rc = quiesce(c)) return rc;  // no trace in flight reads the buffers replaced below
-    c->has_scene = false;
-    for (auto& v : c->scene_copy) v.clear();
-
     // ---- spheres
     std::vector<float4> sph(size_t(n_spheres) * 3);
     for (int i = 0; i < n_spheres; ++i) {
@@ -650,6 +646,56 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
                             m.rayMedium.indexOfRefraction);
         mat[5 * i + 4] = f4(bits(m.rayMedium.priority), bits(m.rayMedium.materialID), m.roughness * m.roughness, 0.0f);
     }
+    // Partial re-upload: the triangles and the BVH entries are the last upload's and every mesh keeps its buffer
+    // offsets (objects moved, or materials / spheres changed): the node records, leaves, triangles and normals on the
+    // device stay; only the mesh table (world->local matrices, materials, exact-cull boxes), spheres and materials are
+    // rebuilt and copied.  Same device contents as a full upload of these arrays.
+    bool partial = c->has_scene && same[3] && same[4] && size_t(n_meshes) == c->dev_meshes.size() &&
+                   c->scene_copy[1].size() == bytes_in[1];
+    for (int mi = 0; partial && mi < n_meshes; ++mi) {
+        const HalogenMeshData& o = reinterpret_cast<const HalogenMeshData*>(c->scene_copy[1].data())[mi];
+        partial = o.triangleBufferOffset == meshes[mi].triangleBufferOffset &&
+                  o.accelerationBufferOffset == meshes[mi].accelerationBufferOffset;
+    }
+    if (partial) {
+        std::vector<HgDevMesh> dm = c->dev_meshes;
+        for (int mi = 0; mi < n_meshes; ++mi) {
+            const HalogenMeshData& m = meshes[mi];
+            if (m.materialIndex >= uint32_t(n_materials))
+                return fail(c, HG_E_INVALID, "mesh %d: materialIndex %u out of range", mi, m.materialIndex);
+            std::memcpy(dm[mi].w2l, m.worldToLocal.m, sizeof dm[mi].w2l);
+            dm[mi].material = m.materialIndex;
+            dm[mi].cullable = 0;
+            const uint32_t off = m.accelerationBufferOffset;
+            if (blas[off].triangleCount == 0) {
+                const BVHEntry& A = blas[off + blas[off].indexA];
+                const BVHEntry& B = blas[off + blas[off].indexA + 1];
+                if (mesh_cull_boxes(m.worldToLocal, A, B, dm[mi])) dm[mi].cullable = 1;
+            }
+        }
+        if (int rc = set_device(c)) return rc;
+        if (int rc = quiesce(c)) return rc;  // no trace in flight reads the buffers replaced below
+        c->has_scene = false;
+        int rc;
+        if ((rc = upload(c, c->spheres, sph.data(), sph.size() * sizeof(float4)))) return rc;
+        if ((rc = upload(c, c->materials, mat.data(), mat.size() * sizeof(float4)))) return rc;
+        if ((rc = upload(c, c->meshes, dm.data(), dm.size() * sizeof(HgDevMesh)))) return rc;
+        for (int k = 0; k < 3; ++k) copy_bytes(c->scene_copy[k], src[k], bytes_in[k]);
+        HG_HIP(c, hipStreamSynchronize(c->stream));
+        c->dev_meshes.swap(dm);
+        c->scene_uploads++;
+        c->scene_uploads_partial++;
+        c->n_spheres = n_spheres;
+        c->n_meshes = n_meshes;
+        c->n_materials = n_materials;
+        c->has_scene = true;
+        return HG_OK;
+    }
+    if (int rc = set_device(c)) return rc;
+    if (int rc = quiesce(c)) return rc;  // no trace in flight reads the buffers replaced below
+    c->has_scene = false;
+    for (auto& v : c->scene_copy) v.clear();
+
     // ---- triangles (independent per triangle: parallel)
     const size_t nt = size_t(n_tris);
 #if HG_TRI_AOS
@@ -798,6 +844,7 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if ((rc = upload(c, c->normals, nrm.data(), nrm.size() * sizeof(float4)))) return rc;
     // the retained copies the next upload compares against (while the device copies run)
     for (int k = 0; k < 5; ++k) copy_bytes(c->scene_copy[k], src[k], bytes_in[k]);
+    c->dev_meshes = dm;
     HG_HIP(c, hipStreamSynchronize(c->stream));  // host staging vectors die at return
     c->scene_uploads++;
     c->n_spheres = n_spheres;
@@ -1531,6 +1578,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->order_faults = v[18];
     out->scene_uploads = c->scene_uploads;
     out->scene_uploads_skipped = c->scene_uploads_skipped;
+    out->scene_uploads_partial = c->scene_uploads_partial;
     return HG_OK;
 }
 

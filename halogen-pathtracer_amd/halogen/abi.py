@@ -83,7 +83,8 @@ class HgCounters(C.Structure):
                 ("trace_cycles", C.c_uint64), ("shade_cycles", C.c_uint64),
                 ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64),
                 ("exec_fallbacks", C.c_uint64), ("trace_busy_ms", C.c_double), ("order_faults", C.c_uint64),
-                ("scene_uploads", C.c_uint64), ("scene_uploads_skipped", C.c_uint64)]
+                ("scene_uploads", C.c_uint64), ("scene_uploads_skipped", C.c_uint64),
+                ("scene_uploads_partial", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)

@@ -173,6 +173,9 @@ typedef struct hg_counters {
     uint64_t scene_uploads_skipped; /* ... and calls whose five arrays equalled the last upload's byte for byte, which
                                        change nothing and return at once (the reference re-uploads on every camera
                                        move: ClearAccumulation sets ObjectBuffersDirty, RP:262-268, 296-299) */
+    uint64_t scene_uploads_partial; /* ... of scene_uploads, those whose triangles and BVH entries equalled the last
+                                       upload's (objects moved, materials changed): only the mesh table, spheres and
+                                       materials were rebuilt */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -242,7 +245,9 @@ const char* hg_last_error(const hg_ctx* ctx);
 /* Upload the scene buffers (UpdateObjectBuffers, RP:448-509).  Validates every cross-reference
  * (offsets, child indices, material indices) before anything reaches the GPU.  Arrays equal byte for byte to the last
  * successful upload's are detected (a parallel compare against retained host copies) and change nothing: the call
- * returns without touching the device (hg_counters.scene_uploads_skipped). */
+ * returns without touching the device (hg_counters.scene_uploads_skipped).  When only the spheres, the meshes'
+ * matrices / materials or the materials changed (triangles, BVH entries and every mesh's buffer offsets as before),
+ * only those tables are rebuilt (hg_counters.scene_uploads_partial). */
 int hg_upload_scene(hg_ctx* ctx,
                     const HalogenSphere* spheres, int32_t n_spheres,
                     const HalogenMeshData* meshes, int32_t n_meshes,

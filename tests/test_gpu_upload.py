@@ -73,3 +73,34 @@ def test_gpu_changed_reupload_rebuilds(gpu):
             cnt = ctx.counters()
         assert cnt["scene_uploads"] == 2 and cnt["scene_uploads_skipped"] == 0, cnt
         assert_bitwise(img, want, "after a changed re-upload")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dragon1_64x36", "glass_64x36"])
+def test_gpu_partial_reupload_equals_full(gpu, name):
+    """An object moved (one mesh's world->local matrix), a material and a sphere changed, the triangles and BVH entries
+    as before: only the mesh table, spheres and materials are rebuilt (hg_counters.scene_uploads_partial), and the
+    render equals a fresh context's full upload of the same arrays, bit for bit."""
+    packed, params, cube, frames, acc = cases.setup(name)
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    moved = _copy(packed)
+    moved.meshes[0].worldToLocal.m[12] += np.float32(0.05)  # translate the first mesh
+    moved.materials[0].roughness = np.float32(0.25)
+    if len(moved.spheres):
+        moved.spheres[0].radius = np.float32(moved.spheres[0].radius * 0.9)
+    want, wcnt = gpu_render(moved, params, 3, True, cube)
+    with abi.Context(0) as ctx:
+        ctx.upload_scene(packed)
+        if cube is not None:
+            ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+        ctx.resize(W, H)
+        ctx.set_params(params)
+        ctx.render(2, True)
+        ctx.upload_scene(moved)
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+        ctx.render(3, True)
+        img = ctx.readback(W, H)
+        cnt = ctx.counters()
+    assert cnt["scene_uploads"] == 2 and cnt["scene_uploads_partial"] == 1 and cnt["scene_uploads_skipped"] == 0, cnt
+    assert_bitwise(img, want, f"{name}: partial re-upload vs a fresh full upload")
