@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel trace + stats of the one-dispatch-per-frame operating point (bench.py --per-frame-only)
 set -u
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=$PWD/gpurun_out/prof
 mkdir -p "$OUT"
 export TMPDIR=/tmp
