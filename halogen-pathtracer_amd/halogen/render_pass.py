@@ -154,12 +154,17 @@ class HalogenRenderPass:
         self._scene_counts = (0, 0)
         self._cubemap_uploaded = False
         self.rank, self.n_ranks = 0, 1
+        # display (RP:343-347): the reference's camera target is R11G11B10 float (URP-HighFidelity.asset:26-27)
+        self.display_format = abi.HG_DISPLAY_R11G11B10F
+        self.display_latency = 1  # frames the shown image lags the traced one (the C# / C++ passes' default)
+        self._display_pending = 0
 
     # ---- RP:237-268 ----------------------------------------------------------------------------
     def OnCameraSetup(self, width: int, height: int):
         res = (int(width), int(height))
         if res != self._prior_resolution:
             self.ctx.resize(*res)
+            self._display_pending = 0  # hg_resize drops the display readbacks in flight
             self.ClearAccumulation()
         self._prior_resolution = res
 
@@ -172,6 +177,7 @@ class HalogenRenderPass:
         """Multi-GPU: render only the 8x8 tiles t with t % n_ranks == rank (not in the reference)."""
         self.rank, self.n_ranks = rank, n_ranks
         self.ctx.set_tiling(rank, n_ranks)
+        self._display_pending = 0
         self.ClearAccumulation()
 
     def UpdateObjectBuffers(self, scene):
@@ -210,6 +216,35 @@ class HalogenRenderPass:
         self.ctx.render(n_frames, accumulate=self.s["Accumulate"])
         if self.s["Accumulate"]:
             self.FrameCount += n_frames
+
+    # ---- the per-frame display (RP:343-347), pipelined, as the C# and C++ passes do it ---------------------------------
+    def set_display(self, fmt: int = abi.HG_DISPLAY_R11G11B10F, latency: int = 1):
+        """Display format (abi.HG_DISPLAY_*) and how many frames the shown image may lag (0..7)."""
+        if not 0 <= latency < abi.HG_READBACK_MAX:
+            raise ValueError("display latency out of range")
+        self.flush_display()
+        self.ctx.set_option(abi.HG_OPT_READBACK_DEPTH, latency + 1)
+        self.display_format, self.display_latency = int(fmt), int(latency)
+
+    def display(self):
+        """Enqueue the display readback of every frame rendered so far; return the image of `display_latency` calls ago
+        (None while the pipeline fills): (h, w) uint32 R11G11B10F, (h, w, 4) float16 or float32."""
+        self.ctx.readback_begin(self.display_format)
+        self._display_pending += 1
+        if self._display_pending <= self.display_latency:
+            return None
+        self._display_pending -= 1
+        w, h = self._prior_resolution
+        return self.ctx.readback_end(w, h)
+
+    def flush_display(self):
+        """The newest display image once the readbacks in flight are done (None when none is)."""
+        last = None
+        w, h = self._prior_resolution or (0, 0)
+        while self._display_pending:
+            self._display_pending -= 1
+            last = self.ctx.readback_end(w, h)
+        return last
 
     def read_image(self) -> np.ndarray:
         w, h = self._prior_resolution

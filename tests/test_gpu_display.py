@@ -83,3 +83,35 @@ def test_gpu_display_format_tiling(gpu):
             img = ctx.readback_end(W, H)
             host = abi.pack_display(np.where(mine[..., None], own, 0).astype(np.float32), fmt)
             assert int((_bits(img) != _bits(host)).sum()) == 0, fmt
+
+
+@pytest.mark.gpu
+def test_gpu_render_pass_display_one_frame_behind(gpu):
+    """The Python HalogenRenderPass's display (as the C# and C++ passes): one Execute per frame, each display() returns
+    the previous frame's R11G11B10F image; a moving camera restarts the accumulation and the display follows."""
+    from halogen import render_pass as rp, scenes
+    cfg = scenes.CONFIGS["C1"].resized(40, 32, 4)
+    scene = cfg.build_scene()
+    cam = cfg.camera()
+    ref = rp.HalogenRenderPass(cfg.settings)
+    want = []
+    for _ in range(4):
+        ref.Execute(scene, cam)
+        want.append(abi.pack_display(ref.read_image(), abi.HG_DISPLAY_R11G11B10F))
+    ref.Dispose()
+    p = rp.HalogenRenderPass(cfg.settings)
+    got = []
+    for _ in range(4):
+        p.Execute(scene, cam)
+        got.append(p.display())
+    assert got[0] is None  # the pipeline fills
+    last = p.flush_display()
+    for k in range(1, 4):
+        assert np.array_equal(got[k], want[k - 1]), k
+    assert np.array_equal(last, want[3])
+    p.set_display(abi.HG_DISPLAY_RGBA16F, 0)  # at once
+    p.Execute(scene, cam)
+    img = p.display()
+    assert img.dtype == np.float16 and np.array_equal(img.view(np.uint16),
+                                                       abi.pack_display(p.read_image(), abi.HG_DISPLAY_RGBA16F).view(np.uint16))
+    p.Dispose()
