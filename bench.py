@@ -166,7 +166,7 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         res = {"bytes_per_frame": W * H * abi.DISPLAY_BPP[fmt]}
         for mode, depth, side in (("sync", 1, 0), ("pipelined", 2, 0), ("pipelined_depth4", 4, 0),
                                   ("pipelined_side", 2, 1), ("pipelined_depth4_side", 4, 1),
-                                  ("pipelined_depth8_side", 8, 1)):
+                                  ("pipelined_depth8_side", 8, 1), ("pipelined_depth16", 16, 0)):
             fresh()
             ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
             ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)
@@ -500,6 +500,8 @@ def main():
                          "never hangs: every hg_comm wait has a deadline)")
     ap.add_argument("--frame-split", type=int, default=-1, help="HG_OPT_FRAME_SPLIT (0 auto, 1 off, k); -1: default")
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
+    ap.add_argument("--wave-units", type=int, default=-1, help="HG_OPT_WAVE_UNITS (0 auto, k tiles per wave); -1: default")
+    ap.add_argument("--lane-pick", type=int, default=-1, help="HG_OPT_LANE_PICK (0 in turn, 1 first idle); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
@@ -555,6 +557,10 @@ def main():
         ctx.set_option(abi.HG_OPT_FRAME_SPLIT, args.frame_split)
     if args.tile_order >= 0:
         ctx.set_option(abi.HG_OPT_TILE_ORDER, args.tile_order)
+    if args.wave_units >= 0:
+        ctx.set_option(abi.HG_OPT_WAVE_UNITS, args.wave_units)
+    if args.lane_pick >= 0:
+        ctx.set_option(abi.HG_OPT_LANE_PICK, args.lane_pick)
     if args.descent_t >= -1:
         ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
@@ -592,13 +598,22 @@ def main():
         ctx.synchronize()
         t0 = time.perf_counter()
         pending = 0
-        for _ in range(args.steps * frames_per_step // args.launch_frames):
+        host = {"render": 0.0, "begin": 0.0, "end": 0.0}  # host time inside each call (the end includes its wait)
+        pc = time.perf_counter
+        n_calls = args.steps * frames_per_step // args.launch_frames
+        for _ in range(n_calls):
+            a = pc()
             ctx.render(args.launch_frames, True)
+            b = pc()
+            host["render"] += b - a
             if args.display != "none":
                 ctx.readback_begin(fmt)
+                e = pc()
+                host["begin"] += e - b
                 pending += 1
                 if pending == depth:
                     ctx.readback_end(W, H, copy=False)
+                    host["end"] += pc() - e
                     pending -= 1
         while pending:
             ctx.readback_end(W, H, copy=False)
@@ -608,7 +623,8 @@ def main():
         c = ctx.counters()
         print(json.dumps({"per_frame_only": True, "value": W * H * frames_per_step * args.steps / dt / 1e6,
                           "unit": "Mpaths/s", "launches": c["launches"], "ms_per_step": dt * 1e3 / args.steps,
-                          "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1)}), flush=True)
+                          "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1),
+                          "host_ms_per_call": {k: v * 1e3 / n_calls for k, v in host.items()}}), flush=True)
         ctx.close()
         return
     for _ in range(args.warmup):

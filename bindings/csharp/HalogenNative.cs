@@ -73,8 +73,9 @@ public static class HalogenNative
                      HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5;
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
-                     HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11;
-    public const int HG_READBACK_MAX = 8;
+                     HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
+                     HG_OPT_LANE_PICK = 14;
+    public const int HG_READBACK_MAX = 16;
     // display formats of hg_readback_begin_format / hg_comm_readback_begin: 16 / 8 / 4 bytes per pixel; R11G11B10F is
     // the URP HDR camera target the reference blits into (GraphicsFormat.B10G11R11_UFloatPack32: R in bits 0-10)
     public const int HG_DISPLAY_RGBA32F = 0, HG_DISPLAY_RGBA16F = 1, HG_DISPLAY_R11G11B10F = 2;

@@ -91,6 +91,8 @@ struct hg_ctx {
     int n_cu = 0;
     int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0, refill = 32;
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
+    int32_t wave_units = 0;   // HG_OPT_WAVE_UNITS, 0: automatic (see hg_render)
+    int32_t lane_pick = HG_LANE_PICK;  // HG_OPT_LANE_PICK: 1-frame chunks on the first idle trace stream (1) or in turn (0)
     int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
     int32_t tile_order_on = HG_TILE_ORDER;  // HG_OPT_TILE_ORDER
     // Render coalescing (HG_OPT_COALESCE): hg_render is asynchronous, so consecutive calls with the same parameters are

@@ -196,6 +196,16 @@
 #ifndef HG_READBACK_SIDE
 #define HG_READBACK_SIDE 0  // default HG_OPT_READBACK_STREAM (display copies on a side stream)
 #endif
+#ifndef HG_WAVE_UNITS_MAX
+#define HG_WAVE_UNITS_MAX 1     // streaming launches without the queue: at most this many tiles per wave (automatic)
+#endif
+#ifndef HG_WAVE_UNITS_ROUNDS
+#define HG_WAVE_UNITS_ROUNDS 3  // ... while the launch keeps at least this many waves per resident wave slot
+#endif
+#ifndef HG_LANE_PICK
+#define HG_LANE_PICK 1  // default HG_OPT_LANE_PICK (display one frame behind +5 %, strict -0.5 %: sweep_r04_depth)
+#endif
+#define HG_WAVE_UNITS_LIMIT 4  // HG_OPT_WAVE_UNITS range (the units' tiles sit in scalar registers)
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif
@@ -271,6 +281,9 @@ struct HgKernelParams {
     // the number of persistent waves (one per resident wave slot of the GPU)
     uint32_t* __restrict__ queue;
     uint32_t resident_waves;
+    // streaming launches without the queue and without a frame split: each wave traces wave_units consecutive units
+    // of the cost order (1: one tile per wave), its lanes taking their items one after another (UnitItems)
+    uint32_t wave_units;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane

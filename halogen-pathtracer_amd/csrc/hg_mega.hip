@@ -230,6 +230,121 @@ struct TileItems {
     }
 };
 
+// LDS words read / written by different lanes of the wave (see the queue's note below)
+__device__ __forceinline__ uint32_t lds_get(uint32_t& x) {
+    return __hip_atomic_load(&x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_put(uint32_t& x, uint32_t v) {
+    __hip_atomic_store(&x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (pixel, frame) items of a streaming wave's units (launches without the queue).  The wave traces the nu units
+// [u0, u0 + nu) of the launch's unit order (wave_unit; nu = kp.wave_units <= HG_WAVE_UNITS_LIMIT, more than one only
+// without a frame split, where unit u is tile ordered_tile(u) with all the launch's frames), their items numbered one
+// unit after another and pixel-major within a unit as in TileItems.  A lane that finishes a frame takes the wave's
+// next item whichever unit holds it, so the wave's lanes drain once per nu tiles instead of once per tile; which wave
+// traces an item changes nothing (every item runs with its own pixel's and frame's inputs and writes its own colour
+// slot).  A lane's item is held as v = unit j << 6 | pixel (x + 8 y); the units' tiles and image origins sit in the
+// wave's LDS (the kernel's scalar registers are all taken), read once when a path starts and once when it ends.
+__shared__ uint32_t hg_unit_tile[HG_WAVE_UNITS_LIMIT];  // unit j's local tile
+__shared__ uint32_t hg_unit_org[HG_WAVE_UNITS_LIMIT];   // its image origin x | y << 16
+__shared__ uint32_t hg_unit_shape;                      // unit 0's valid width | valid pixels << 8
+struct UnitItems {
+    uint32_t nu, nf, f_begin, n_items, full;  // wave-uniform (scalar registers)
+    __device__ UnitItems() : nu(0), nf(1), f_begin(0), n_items(0), full(1) {}  // unused (kQueue)
+    __device__ UnitItems(const HgKernelParams& kp, uint32_t u_first, int first_tile, bool valid, uint32_t fb,
+                         uint32_t fe, uint32_t lane) {
+        const uint32_t nlt = uint32_t(kp.n_local_tiles), u0 = __builtin_amdgcn_readfirstlane(u_first);
+        nu = valid ? (kp.wave_units > 1u && u0 < nlt ? min(min(kp.wave_units, uint32_t(HG_WAVE_UNITS_LIMIT)), nlt - u0)
+                                                     : 1u)
+                   : 0u;
+        nu = __builtin_amdgcn_readfirstlane(nu);
+        nf = __builtin_amdgcn_readfirstlane(fe > fb ? fe - fb : 1u);
+        f_begin = fb;
+        n_items = 0u;
+        full = 1u;
+        for (uint32_t j = 0; j < nu; ++j) {
+            const uint32_t t = __builtin_amdgcn_readfirstlane(j == 0u ? first_tile : ordered_tile(kp, u0 + j));
+            uint32_t tx0, ty0, tw, th;
+            tile_rect(kp, t, tx0, ty0, tw, th);
+            if (lane == 0) {
+                hg_unit_tile[j] = t;
+                hg_unit_org[j] = tx0 | (ty0 << 16);
+                if (j == 0u) hg_unit_shape = tw | ((tw * th) << 8);
+            }
+            n_items += tw * th * (fe > fb ? fe - fb : 0u);
+            full &= tw * th == 64u ? 1u : 0u;
+        }
+        n_items = __builtin_amdgcn_readfirstlane(n_items);
+        full = __builtin_amdgcn_readfirstlane(full);
+        if (lane == 0) hg_next_item = 64u;  // lane l starts with item l
+        wave_lds_sync();
+    }
+    __device__ static __forceinline__ void tile_rect(const HgKernelParams& kp, uint32_t t, uint32_t& tx0, uint32_t& ty0,
+                                                     uint32_t& tw, uint32_t& th) {
+        const uint32_t g = uint32_t(kp.rank) + t * uint32_t(kp.n_ranks);
+        const uint32_t ty = g / uint32_t(kp.tiles_x);
+        tx0 = (g - ty * uint32_t(kp.tiles_x)) * HG_TILE;
+        ty0 = ty * HG_TILE;
+        tw = min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0));
+        th = min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0));
+    }
+    // item k -> v (unit j << 6 | pixel) and its frame
+    __device__ __forceinline__ void get(const HgKernelParams& kp, uint32_t k, uint32_t& v, uint32_t& frame) const {
+        uint32_t j = 0u, kk = k, nv = 64u, tw = 8u;
+        if (full) {
+            if ((nf & (nf - 1u)) == 0u) {
+                const uint32_t lg = 6u + uint32_t(__builtin_ctz(nf));
+                j = k >> lg;
+                kk = k & ((1u << lg) - 1u);
+            } else {
+                j = k / (64u * nf);
+                kk = k - j * (64u * nf);
+            }
+        } else {  // a tile at the image edge (only ever a wave's one unit: the runtime gives such images one tile per wave)
+            const uint32_t sh = lds_get(hg_unit_shape);
+            tw = sh & 0xFFu;
+            nv = sh >> 8;
+        }
+        uint32_t i, f;
+        if ((nf & (nf - 1u)) == 0u) {
+            const uint32_t lg = uint32_t(__builtin_ctz(nf));
+            i = kk >> lg;
+            f = kk & (nf - 1u);
+        } else {
+            i = kk / nf;
+            f = kk - i * nf;
+        }
+        v = (j << 6) | (nv == 64u ? i : (i % tw) + 8u * (i / tw));
+        frame = f_begin + f;
+    }
+    __device__ __forceinline__ uint32_t slot(uint32_t v) const {
+        return nu <= 1u ? (lds_get(hg_unit_tile[0]) * 64u + v) : lds_get(hg_unit_tile[v >> 6]) * 64u + (v & 63u);
+    }
+    __device__ __forceinline__ void pixel(uint32_t v, uint32_t& x, uint32_t& y) const {
+        const uint32_t o = lds_get(hg_unit_org[v >> 6]);
+        x = (o & 0xFFFFu) + (v & 7u);
+        y = (o >> 16) + ((v >> 3) & 7u);
+    }
+    __device__ __forceinline__ uint32_t take_here() const {
+        const uint64_t m = __builtin_amdgcn_read_exec();
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        uint32_t base = 0;
+        if (rank == 0u) base = atomicAdd(&hg_next_item, uint32_t(__builtin_popcountll(m)));
+        base = __builtin_amdgcn_readfirstlane(base);
+        return base + rank;
+    }
+    // the wave's clock since tile_cost_begin, shared out over its units' tiles (the first one's pointer is in LDS)
+    __device__ __forceinline__ void record_cost(const HgKernelParams& kp, uint32_t lane) const {
+        if (nu <= 1u) {
+            record_tile_cost(lane);
+            return;
+        }
+        if (lane != 0 || !hg_wave_cost[threadIdx.x >> 6]) return;
+        const uint64_t share = (wave_clock() - hg_wave_t0[threadIdx.x >> 6]) / nu;
+        for (uint32_t j = 0; j < nu; ++j) cost_add(kp.tile_cost + lds_get(hg_unit_tile[j]), share);
+    }
+};
+
 // Cost order (hg_render, per trace stream): tile_order = the local tiles, most expensive first, then the costs are
 // cleared for the next launches.  A counting sort over 1024 log-scale cost buckets (16 per octave of the wave-clock
 // cost: bucket 0 the most expensive; two tiles share one only within ~4 % of each other), in two launches of one-wave
@@ -717,12 +832,6 @@ hipError_t hg_launch_mega_regen(const HgKernelParams& kp_in, int block, bool cou
 // LDS words read / written by different lanes of the wave: relaxed workgroup-scope atomics on the __shared__ object
 // itself compile to plain ds_read / ds_write that the compiler may not cache in registers (a volatile access through
 // a cast pointer became a FLAT access with a 64-bit generic address and cost the kernel 60 B of scratch)
-__device__ __forceinline__ uint32_t lds_get(uint32_t& x) {
-    return __hip_atomic_load(&x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_put(uint32_t& x, uint32_t v) {
-    __hip_atomic_store(&x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 constexpr uint32_t kFreshLane = 0xFFFFFFFFu;  // `bounce` of a lane that has no path yet (it takes its item when shading)
 // The wave's two current units (double-buffered), in LDS (one wave per workgroup).  Item numbers (hg_next_item) run on
 // across units: unit hg_q_cur covers [base, end), the other one the numbers after it, so a lane whose take runs past
@@ -885,7 +994,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
     const uint32_t n_units = nlt * split;  // kQueue: (tile, frame chunk) units of the queue
     int local_tile = 0;
-    uint32_t chunk = 0, f_begin = 0, f_end = 0;
+    uint32_t chunk = 0, f_begin = 0, f_end = 0, u_first = 0;
     if constexpr (kQueue) {
         if (lane == 0) {
             lds_put(hg_next_item, 0u);
@@ -901,7 +1010,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
         // one wave per workgroup (launched with 64 threads): wave = workgroup
         const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
-        wave_unit(kp, gw, nlt, split, local_tile, chunk);
+        u_first = gw * (kp.wave_units > 1u ? kp.wave_units : 1u);  // (more than one unit only without a frame split)
+        wave_unit(kp, u_first, nlt, split, local_tile, chunk);
         tile_cost_begin(kp, lane, local_tile, chunk < split);
         f_begin = uint32_t((uint64_t(chunk) * uint32_t(kp.n_frames)) / split);
         f_end = uint32_t((uint64_t(chunk + 1) * uint32_t(kp.n_frames)) / split);
@@ -936,18 +1046,16 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     float acc_rough = 0.0f;
     Trav tv;
     tv.mi = nm;
-    uint32_t slot = 0;  // kQueue: the lane's item's accumulator slot (local tile * 64 + pixel)
+    uint32_t slot = 0;  // the lane's item: kQueue its accumulator slot (local tile * 64 + pixel), else v (UnitItems)
     bool dry = false;   // kQueue, wave-uniform: the queue has no unit left
-    uint32_t pix = lane;  // otherwise: the item's pixel within the wave's tile (x + 8 y)
-    const TileItems items = kQueue ? TileItems() : TileItems(kp, local_tile, chunk < split, f_begin, f_end, lane);
+    const UnitItems items = kQueue ? UnitItems() : UnitItems(kp, u_first, local_tile, chunk < split, f_begin, f_end, lane);
     if constexpr (kQueue) {
         wave_lds_sync();  // hg_q / hg_next_item initialised (lane 0); every lane takes its first item in the loop
     } else {
         if (lane < items.n_items) {  // item `lane`
             uint32_t f;
-            items.get(lane, pix, f);
-            px = items.tx0 + (pix & 7u);
-            py = items.ty0 + (pix >> 3);
+            items.get(kp, lane, slot, f);
+            items.pixel(slot, px, py);
             fs = f << 16;
             smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(px + py * kp.Wu), 0u};
         }
@@ -1057,7 +1165,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 bool next = !fresh && (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
                 if (!next) {
                     const f3 color = sample_mean(kp, sum);
-                    const size_t slot_i = kQueue ? size_t(slot) : size_t(uint32_t(local_tile)) * 64u + pix;
+                    const size_t slot_i = kQueue ? size_t(slot) : size_t(items.slot(slot));
                     // this frame's colour, blended later in frame order (hg_blend_frames)
 #if !HG_DIAG_NO_FC  // (analysis builds only: the write-traffic attribution of DESIGN.md §4.5)
                     if (!fresh)
@@ -1077,13 +1185,14 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     } else {
                         const uint32_t k = items.take_here();
                         if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
-                            uint32_t f;
-                            items.get(k, pix, f);
+                            uint32_t f, hx, hy;
+                            items.get(kp, k, slot, f);
+                            items.pixel(slot, hx, hy);
                             next = true;
                             sum = mk(0, 0, 0);
                             fs = f << 16;
-                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u,
-                                          pcg_hash(items.tx0 + (pix & 7u) + (items.ty0 + (pix >> 3)) * kp.Wu), 0u};
+                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
+                                          0u};
                             ms = MediumStack{0ull, 0};
                         }
                     }
@@ -1092,12 +1201,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 if (next) {
                     {
                         uint32_t qx, qy;
-                        if constexpr (kQueue) {
-                            slot_pixel(kp, slot, qx, qy);
-                        } else {
-                            qx = items.tx0 + (pix & 7u);
-                            qy = items.ty0 + (pix >> 3);
-                        }
+                        if constexpr (kQueue) slot_pixel(kp, slot, qx, qy);
+                        else items.pixel(slot, qx, qy);
                         ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
                     }
                     thr = mk(1, 1, 1);
@@ -1152,8 +1257,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                     ms.s = (uint64_t(bperm(src, uint32_t(ms.s >> 32))) << 32) | bperm(src, uint32_t(ms.s));
                     ms.sp = int(bperm(src, uint32_t(ms.sp)));
                     acc_rough = bpermf(src, acc_rough);
-                    if constexpr (kQueue) slot = bperm(src, slot);
-                    else pix = bperm(src, pix);
+                    slot = bperm(src, slot);
                     const RowVec3<kRowThr> o_thr{src};
                     const RowVec3<kRowCol> o_col{src};
                     const f3 t_thr = o_thr.get(), t_col = o_col.get();
@@ -1176,7 +1280,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #endif
         if (kCounters) cyc_shade += wave_clock();
     }
-    record_tile_cost(lane);
+    if constexpr (kQueue) record_tile_cost(lane);
+    else items.record_cost(kp, lane);
     if constexpr (kQueue) {
         // The last wave out resets the queue heads for the next launch on this stream (no memset launch per queue
         // launch: a blit kernel waited for a CU that the other streams' persistent waves held).  A wave leaves only
@@ -1216,6 +1321,8 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
     const bool queue = kp_in.queue != nullptr;  // the runtime passes a queue for launches of few frames
     if (queue) grid = grid < int64_t(kp_in.resident_waves) ? grid : int64_t(kp_in.resident_waves);  // persistent waves
+    else if (kp_in.wave_units > 1u && kp_in.frame_split == 1)  // wave_units tiles per wave (UnitItems)
+        grid = (grid + kp_in.wave_units - 1) / kp_in.wave_units;
     if (grid == 0) return hipSuccess;
     const uint32_t lds_depth = kp_in.stack_depth < HG_STREAM_LDS_STACK ? kp_in.stack_depth : HG_STREAM_LDS_STACK;
     const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t) + HG_STREAM_LDS_PAD;

@@ -1157,8 +1157,16 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 // two others cost C3 1.5 %)
                 int li;
                 if (kc.n_frames <= HG_QUEUE_MAX_FRAMES) {
-                    li = c->next_lane;
-                    c->next_lane = (c->next_lane + 1) % HG_TRACE_LANES;
+                    li = -1;
+                    if (c->lane_pick) {  // the first stream whose last trace and blend are done (its queue stays warm)
+                        for (int j = 0; j < HG_TRACE_LANES && li < 0; ++j)
+                            if (!c->lanes[j].blend_pending || hipEventQuery(c->lanes[j].blended) == hipSuccess) li = j;
+                        (void)hipGetLastError();  // hipErrorNotReady is a status here
+                    }
+                    if (li < 0) {
+                        li = c->next_lane;
+                        c->next_lane = (c->next_lane + 1) % HG_TRACE_LANES;
+                    }
                 } else {
                     li = c->next_lane_big;
                     c->next_lane_big = (c->next_lane_big + 1) % HG_TRACE_LANES_BIG;
@@ -1181,6 +1189,16 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                         if (&O != &L && O.blend_pending && hipEventQuery(O.traced) == hipErrorNotReady) ++busy;
                     (void)hipGetLastError();  // hipErrorNotReady is a status here, not an error for the launch check
                     if (busy >= 2) kc.resident_waves = slots / uint32_t(std::min(HG_QUEUE_WAVES_DIV, busy + 1));
+                }
+                // Streaming launches without the queue and without a frame split: each wave traces wave_units
+                // consecutive tiles of the cost order, its lanes draining once per wave instead of once per tile
+                // (UnitItems), while the launch keeps at least HG_WAVE_UNITS_ROUNDS waves per resident slot
+                kc.wave_units = 1;
+                // (whole tiles only: a wave's units are all 8 x 8, UnitItems)
+                if (stream_k && !kc.queue && kc.frame_split == 1 && tiles > 0 && c->W % HG_TILE == 0 &&
+                    c->H % HG_TILE == 0) {
+                    const int64_t auto_wu = std::min<int64_t>(HG_WAVE_UNITS_MAX, tiles / (int64_t(HG_WAVE_UNITS_ROUNDS) * slots));
+                    kc.wave_units = uint32_t(c->wave_units > 0 ? c->wave_units : std::max<int64_t>(1, auto_wu));
                 }
                 kc.tile_order = nullptr;
                 kc.tile_cost = ordered ? static_cast<unsigned long long*>(L.tile_cost.p) : nullptr;
@@ -1658,6 +1676,14 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");
             c->frame_split = value;
+            return HG_OK;
+        case HG_OPT_LANE_PICK:
+            c->lane_pick = value ? 1 : 0;
+            return HG_OK;
+        case HG_OPT_WAVE_UNITS:
+            if (value < 0 || value > HG_WAVE_UNITS_LIMIT)
+                return fail(c, HG_E_INVALID, "wave units must be 0 (auto)..%d", HG_WAVE_UNITS_LIMIT);
+            c->wave_units = value;
             return HG_OK;
         default:
             return fail(c, HG_E_INVALID, "unknown option %d", option);

@@ -100,7 +100,9 @@ HG_OPT_TILE_ORDER = 8
 HG_OPT_COALESCE = 9
 HG_OPT_READBACK_DEPTH = 10
 HG_OPT_READBACK_STREAM = 11
-HG_READBACK_MAX = 8
+HG_OPT_WAVE_UNITS = 12
+HG_OPT_LANE_PICK = 14
+HG_READBACK_MAX = 16
 # display formats of readback_begin(format=...) (include/halogen_abi.h, csrc/hg_pack.h): bytes per pixel and numpy view
 HG_DISPLAY_RGBA32F, HG_DISPLAY_RGBA16F, HG_DISPLAY_R11G11B10F = 0, 1, 2
 DISPLAY_FORMATS = {"rgba32f": HG_DISPLAY_RGBA32F, "rgba16f": HG_DISPLAY_RGBA16F, "r11g11b10f": HG_DISPLAY_R11G11B10F}

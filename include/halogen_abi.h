@@ -224,17 +224,22 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   (each launches the held frames first).  The frames, their order and the image are those of separate launches; a
  *   launch has a fixed cost (its drain tail: ~0.35 ms on C3), so the reference's one call per frame (RP:327) runs at
  *   the multi-frame rate.  1 = every call launches at once. */
-/* HG_OPT_READBACK_DEPTH: display readbacks (hg_readback_begin[_format]) that may be outstanding at once, 1..8
+/* HG_OPT_READBACK_DEPTH: display readbacks (hg_readback_begin[_format]) that may be outstanding at once, 1..16
  *   (default 2: display one frame behind).  A deeper ring lets a caller that displays every frame keep more frames in
  *   flight (display latency traded for throughput); changing it needs no readback outstanding. */
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
-       HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11 };
+       HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
+       HG_OPT_LANE_PICK = 14 };
 /* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
  *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
  *   device image and copied on the context stream.  Same images either way. */
-#define HG_READBACK_MAX 8
-
+#define HG_READBACK_MAX 16
+/* HG_OPT_WAVE_UNITS: streaming launches of more than 8 frames without a frame split, tiles traced per wave (1..4;
+ *   0 = automatic, which is 1: more tiles per wave measured slower).  Images whose size is not
+ *   a multiple of 8 always trace one tile per wave.  Same images and counters either way.
+ * HG_OPT_LANE_PICK (default 1): launches of at most 8 frames go to the first trace stream whose previous trace and blend are done
+ *   (1), or to the trace streams in turn (0).  Same images either way. */
 int hg_abi_version(void);
 
 /* Create a context on HIP device `device` (ordinal as seen by the process). */

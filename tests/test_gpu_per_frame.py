@@ -236,3 +236,39 @@ def test_gpu_display_readback_tiling_and_resize(gpu):
         ctx.resize(W // 2, H)  # drops the outstanding readback (and its image)
         with pytest.raises(abi.HalogenError, match="no readback outstanding"):
             ctx.readback_end(W // 2, H)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lane_pick", [0, 1])
+def test_gpu_display_deep_ring(gpu, lane_pick):
+    """Up to HG_READBACK_MAX (16) display readbacks outstanding, every call its own 1-frame launch, on the first idle
+    trace stream (HG_OPT_LANE_PICK 1, the default) or on the streams in turn: each displayed image equals the image of
+    that many frames."""
+    assert abi.HG_READBACK_MAX == 16
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    n = 20
+    want = [gpu_render(packed, params, k, True, cube)[0] for k in range(1, n + 1)]
+    with abi.Context(0) as ctx:
+        ctx.set_option(abi.HG_OPT_LANE_PICK, lane_pick)
+        ctx.set_option(abi.HG_OPT_COALESCE, 1)
+        ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 16)
+        with pytest.raises(abi.HalogenError, match="readback depth"):
+            ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 17)
+        ctx.upload_scene(packed)
+        ctx.resize(W, H)
+        ctx.set_params(params)
+        got, pending = [], 0
+        for _ in range(n):
+            ctx.render(1, True)
+            ctx.readback_begin()
+            pending += 1
+            if pending == 16:
+                got.append(ctx.readback_end(W, H))
+                pending -= 1
+        while pending:
+            got.append(ctx.readback_end(W, H))
+            pending -= 1
+        assert len(got) == n
+        for k, img in enumerate(got):
+            assert_bitwise(img, want[k], f"display ring of 16, frame {k + 1}, lane pick {lane_pick}")

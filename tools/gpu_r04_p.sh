@@ -1,0 +1,9 @@
+#!/bin/bash
+# the whole GPU suite on the current library
+set -u
+mkdir -p gpurun_out
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_p.log 2>&1; rc=$?
+echo "smoke rc=$rc"; tail -1 gpurun_out/smoke_p.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests \
+    > gpurun_out/pytest_p.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_p.log; exit $rc
