@@ -580,8 +580,26 @@ def main():
         dist.broadcast_object_list(box, src=0)
         return abi.Comm.rank(ctx, world, box[0], rank)
 
+    comm_init_error = None
     if dist is not None and gather_mode == "abi":
-        comm = join_comm()
+        # Every rank joins; if any rank's join fails (bounded by the comm deadline), all of them agree to time the torch
+        # gather instead and the line says why (`gather_init_error`), so a broken hg_comm never costs the measurement.
+        try:
+            comm = join_comm()
+        except abi.HalogenError as e:
+            comm_init_error = f"rank {rank}: {str(e)[:300]}"
+        import torch
+
+        bad = torch.tensor([1 if comm_init_error else 0], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if int(bad.item()):
+            errs = [None] * world
+            dist.all_gather_object(errs, comm_init_error)
+            comm_init_error = "; ".join(e for e in errs if e) or "a peer failed to join"
+            if comm is not None:
+                comm.close()
+                comm = None
+            gather_mode = "torch"
     setup_s = time.perf_counter() - t_setup
 
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
@@ -674,7 +692,7 @@ def main():
 
     abi_check = None
     gather_ms = {}
-    if dist is not None and not args.no_abi_check:
+    if dist is not None and not args.no_abi_check and comm_init_error is None:
         import torch
 
         from halogen import distributed as hd
@@ -814,6 +832,7 @@ def main():
                                       "hg_comm_assemble_host's pixel index)"))
             if dist is not None else None,
             "abi_gather_check": abi_check,
+            "gather_init_error": comm_init_error,
             # each gather alone (after the timed region; max over ranks): the one `gather` names is inside `value`
             "gather_ms": gather_ms or None,
             "setup_s": setup_s,

@@ -21,3 +21,16 @@ same = a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32
 print('n=$n gathered image bit-identical to 1-rank render:', same, a.shape)
 sys.exit(0 if same else 1)" || exit 1
 done
+# the default transport (hg_comm over RCCL) cannot join two ranks on one GPU (RCCL refuses a duplicate device): every
+# rank must agree to time the torch gather instead, report why, and still gather the same image
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29510 bench.py --gpus 2 --dist-backend gloo $ARGS --save-image gpurun_out/dist/img_abi2.npy \
+    > gpurun_out/dist/bench_abi2.json 2> gpurun_out/dist/bench_abi2.err
+rc=$?; echo "n=2 abi fallback rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dist/bench_abi2.err; exit $rc; }
+python -c "
+import json, numpy as np, sys
+r = json.loads(open('gpurun_out/dist/bench_abi2.json').read().strip().splitlines()[-1])
+a = np.load('gpurun_out/dist/img_abi2.npy'); b = np.load('gpurun_out/dist/img_1x2.npy')
+same = np.array_equal(a.view(np.uint32), b.view(np.uint32))
+print('gather:', r['gather'], '| init error:', (r['gather_init_error'] or '')[:160], '| bit-identical:', same)
+sys.exit(0 if same and r['gather_init_error'] else 1)" || exit 1
