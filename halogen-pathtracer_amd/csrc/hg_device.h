@@ -1009,6 +1009,65 @@ __device__ __forceinline__ bool quad_node_fetch(const HgKernelParams& kp, bool w
 }
 #endif
 
+#if HG_NODE_DEDUP
+// Wave-level deduplicated node fetch (DESIGN.md §10 lever 10).  A descent round's loading lanes need few distinct
+// records (C3: 5-16 in 48 % of rounds, 17-32 in 47 %, more in 0.07 %; tools/coherence_stats.py), yet each lane
+// loading its own 64-B record costs the texture-data unit four wave instructions whatever the sharing.  Here the
+// distinct records are enumerated (one readlane + ballot per record), packed densely into lanes (4 lanes x 16 B per
+// record when at most 16, else 2 lanes x 2 x 16 B), fetched with one or two wave instructions, and every lane takes
+// its record's 16 words from their lanes with ds_bpermute.  The same bytes: the same results.  Returns false (the
+// caller loads per lane) when more than 32 records are needed.  The whole wave must be active.
+__device__ __forceinline__ uint32_t bperm_u(uint32_t src_lane, uint32_t v) {
+    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src_lane << 2), int(v)));
+}
+__device__ __forceinline__ float4 bperm_f4(uint32_t src_lane, const float4& v) {
+    const int a = int(src_lane << 2);
+    return make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.x))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.y))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.z))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.w))));
+}
+__device__ __forceinline__ bool wave_node_fetch(const HgKernelParams& kp, bool want, uint32_t node, NodePair& np) {
+    const uint32_t lane = __lane_id();
+    uint64_t m = wave_ballot(want);
+    uint32_t slot = 0u, list = 0u, k = 0u;
+    while (m != 0ull && k < 32u) {  // wave-uniform: one distinct record per iteration
+        const uint32_t first = uint32_t(__builtin_amdgcn_readlane(int(node), int(__builtin_ctzll(m))));
+        const bool same = want && node == first;
+        m &= ~wave_ballot(same);
+        slot = same ? k : slot;
+        list = lane == k ? first : list;
+        ++k;
+    }
+    if (m != 0ull) return false;
+    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (k <= 16u) {  // record j in lanes 4j .. 4j+3, 16 B each: one load instruction
+        const uint32_t rec = bperm_u(lane >> 2, list);
+        float4 a = z;
+        if ((lane >> 2) < k) a = ld_off(kp.nodes, (rec << 6) + ((lane & 3u) << 4));
+        const uint32_t s = slot << 2;
+        np.q0 = bperm_f4(s, a);
+        np.q1 = bperm_f4(s + 1u, a);
+        np.q2 = bperm_f4(s + 2u, a);
+        np.q3 = bperm_f4(s + 3u, a);
+    } else {  // record j in lanes 2j, 2j+1: bytes 0-15 / 16-31 (first load), 32-47 / 48-63 (second)
+        const uint32_t rec = bperm_u(lane >> 1, list);
+        float4 a = z, b = z;
+        if ((lane >> 1) < k) {
+            const uint32_t off = (rec << 6) + ((lane & 1u) << 4);
+            a = ld_off(kp.nodes, off);
+            b = ld_off(kp.nodes, off + 32u);
+        }
+        const uint32_t s = slot << 1;
+        np.q0 = bperm_f4(s, a);
+        np.q1 = bperm_f4(s + 1u, a);
+        np.q2 = bperm_f4(s, b);
+        np.q3 = bperm_f4(s + 1u, b);
+    }
+    return true;
+}
+#endif
+
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
@@ -1072,16 +1131,34 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     uint64_t dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     while (dm != 0ull && (uint32_t(__builtin_popcountll(dm)) > dt || dm == act_mask)) {
         c.node_rounds += wave_once();
-#if HG_QUAD_FETCH && !HG_NODE_CACHE
+#if HG_COHERENCE_STATS  // analysis builds: distinct node records among the loading lanes, into shade_detail[0..3]
+        if (kp.counters) {  // buckets: 1-4 / 5-16 / 17-32 / more than 32 distinct records per node round
+            uint64_t m = dm;
+            uint32_t k = 0;
+            while (m != 0ull) {
+                const uint32_t first = uint32_t(__builtin_amdgcn_readlane(int(t.node), int(__builtin_ctzll(m))));
+                m &= ~wave_ballot(t.node == first);
+                ++k;
+            }
+            const int slot = k <= 4u ? 11 : k <= 16u ? 12 : k <= 32u ? 13 : 14;
+            if (int(threadIdx.x & 63u) == __ffsll((unsigned long long)__ballot(1)) - 1)
+                atomicAdd(kp.counters + slot, 1ull);
+        }
+#endif
+#if (HG_QUAD_FETCH || HG_NODE_DEDUP) && !HG_NODE_CACHE
         const bool want = act && int32_t(t.node) >= 0;
         NodePair np;
+#if HG_NODE_DEDUP
+        const bool coop = wave_node_fetch(kp, want, t.node, np);
+#else
         const bool coop = quad_node_fetch(kp, want, t.node, np.q0, np.q1, np.q2, np.q3);
+#endif
         if (want) {
             if (!coop) np = node_pair(kp, t.node);
 #else
         if (act && int32_t(t.node) >= 0) {
 #endif
-#if HG_QUAD_FETCH && !HG_NODE_CACHE
+#if (HG_QUAD_FETCH || HG_NODE_DEDUP) && !HG_NODE_CACHE
 #elif HG_NODE_CACHE
             // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
             const NodePair np = t.node < kp.hot_records

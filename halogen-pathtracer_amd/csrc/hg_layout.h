@@ -196,6 +196,12 @@
 #ifndef HG_READBACK_SIDE
 #define HG_READBACK_SIDE 0  // default HG_OPT_READBACK_STREAM (display copies on a side stream)
 #endif
+#ifndef HG_NODE_DEDUP
+#define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
+#endif
+#ifndef HG_COHERENCE_STATS
+#define HG_COHERENCE_STATS 0  // analysis builds: histogram of distinct node records per descent round (hg_device.h)
+#endif
 #ifndef HG_WAVE_UNITS_MAX
 #define HG_WAVE_UNITS_MAX 1     // streaming launches without the queue: at most this many tiles per wave (automatic)
 #endif
