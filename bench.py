@@ -106,6 +106,56 @@ def framed_measurement(ctx, packed, s, W, H, frames_per_step: int, steps: int) -
             "roofline": roofline}
 
 
+def fast_bvh_measurement(ctx, cfg, packed, cube, params, W, H, frames_per_step: int, steps: int, ref_img,
+                         headline: float) -> dict:
+    """The same workload on an SAH hierarchy (hg_build_blas_sah) instead of the reference
+    builder's: NOT the contract line (the drop-in keeps BVHGenerator's tree), a second number beside it.  The kernel
+    traverses any hierarchy the reference's way (tests/test_gpu_fast_bvh.py: bit-exact against the oracle on the same
+    tree), so the images differ only where two triangles tie within rounding; the leg reports how many pixels of the
+    timed region's final image differ from the headline's.  Same loop as the headline: warm-up, `steps` x
+    hg_render(frames_per_step) from a cleared accumulator, then a counting replay step."""
+    from halogen import scene as scene_mod
+
+    prev = scene_mod.set_blas_builder("sah")
+    try:
+        t = time.perf_counter()
+        sah = cfg.build_scene().pack()
+        build_s = time.perf_counter() - t
+    finally:
+        scene_mod.set_blas_builder(prev)
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.upload_scene(sah)
+    ctx.set_params(params)
+    for _ in range(3):
+        ctx.render(frames_per_step, True)
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.render(frames_per_step, True)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    img = ctx.readback(W, H)
+    differ = (img.view(np.uint32) != ref_img.view(np.uint32)).any(-1)
+    d = np.abs(img.astype(np.float64) - ref_img.astype(np.float64))
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.reset_counters()
+    ctx.set_option(abi.HG_OPT_COUNTERS, 1)
+    ctx.render(frames_per_step, True)
+    c = ctx.counters()
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.upload_scene(packed)  # the reference tree again for the legs after this one
+    value = W * H * frames_per_step * steps / dt / 1e6
+    return {"workload": "C3 on an SAH BLAS (hg_build_blas_sah, max leaf 2): not the reference's hierarchy",
+            "value": value, "unit": "Mpaths/s", "steps": steps, "ms_per_step": dt * 1e3 / steps,
+            "frac_of_headline": value / headline, "build_s": build_s, "blas_nodes": len(sah.blas),
+            "pixels_differing_from_headline_image": float(differ.mean()),
+            "max_abs_diff": float(d.max()), "mean_abs_diff": float(d.mean()),
+            "counters_per_path": {k: c[k] / c["paths"] for k in ("rays", "tri_tests", "aabb_tests", "hits")}}
+
+
 def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_value: float) -> dict:
     """The drop-in's operating point: the reference dispatches HalogenCompute once per frame (RP:327, RP:406) and the
     C# shim calls hg_render(ctx, 1, 1) per Execute.  The same C3 step (`frames` progressive frames from a cleared
@@ -502,6 +552,11 @@ def main():
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--wave-units", type=int, default=-1, help="HG_OPT_WAVE_UNITS (0 auto, k tiles per wave); -1: default")
     ap.add_argument("--lane-pick", type=int, default=-1, help="HG_OPT_LANE_PICK (0 in turn, 1 first idle); -1: default")
+    ap.add_argument("--bvh", default="reference", choices=["reference", "sah"],
+                    help="BLAS builder of the timed scene: the reference's (the drop-in's parity path, the contract line) "
+                         "or hg_build_blas_sah (NOT the reference's hierarchy; A/B and the fast_bvh leg)")
+    ap.add_argument("--sah-leaf", type=int, default=2, help="--bvh sah: largest leaf the SAH build makes by size alone")
+    ap.add_argument("--no-fast-bvh", action="store_true", help="skip the fast_bvh leg (C3 on an SAH BLAS)")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
@@ -535,7 +590,12 @@ def main():
     settings = scenes.settings_for(cfg)
     s = rp.clamp_settings(settings)
     t_setup = time.perf_counter()
+    from halogen import scene as scene_mod
+
+    scene_mod.SAH_MAX_LEAF = args.sah_leaf
+    scene_mod.set_blas_builder(args.bvh)
     packed = cfg.build_scene().pack()
+    scene_mod.set_blas_builder("reference")
     cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
     W, H = cfg.width, cfg.height
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
@@ -852,6 +912,10 @@ def main():
             result["camera_move"] = camera_move_measurement(ctx, packed, s, cfg, W, H, 32, cube)
         if world == 1 and not emu and args.config == "C3" and not args.no_counters and not args.no_framed:
             result["framed"] = framed_measurement(ctx, packed, s, W, H, frames_per_step, max(2, args.steps // 4))
+        if (world == 1 and not emu and args.config == "C3" and args.bvh == "reference" and not args.no_fast_bvh
+                and timed_img is not None):
+            result["fast_bvh"] = fast_bvh_measurement(ctx, cfg, packed, cube, params, W, H, frames_per_step, args.steps,
+                                                      timed_img, result["value"])
         if world == 1 and not args.no_cpu_baseline:
             # the box's CPU share is 16 (OMP_NUM_THREADS there); never more threads than CPUs this process may use
             threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")

@@ -117,6 +117,9 @@ public static class HalogenNative
     [DllImport(Lib)] public static extern long hg_build_blas_mt(float[] vertices, int nVertices, int[] indices,
         int nTris, float[] rootMin, float[] rootMax, int maxHierarchyDepth, [Out] BVHEntry[] outNodes, long maxNodes,
         int nThreads);
+    // an SAH hierarchy in the same format: NOT BVHGenerator's tree (a faster render, not the reference's images)
+    [DllImport(Lib)] public static extern long hg_build_blas_sah(float[] vertices, int nVertices, int[] indices,
+        int nTris, int maxLeaf, int maxDepth, [Out] BVHEntry[] outNodes, long maxNodes);
     [DllImport(Lib)] public static extern void hg_unity_bounds(float[] inMin, float[] inMax, int padIfThin,
         [Out] float[] outMin, [Out] float[] outMax);
     [DllImport(Lib)] public static extern int hg_pack_triangles(float[] vertices, float[] normals, int nVertices,

@@ -518,3 +518,168 @@ extern "C" int hg_pack_triangles(const float* V, const float* N, int32_t n_verti
     }
     return HG_OK;
 }
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Fast BLAS ("an SAH variant behind a non-parity flag"): a binned surface-area-heuristic build
+// that emits the reference's BVHEntry format — children of entry g at indexA and indexA + 1, leaves holding a range of
+// the reordered triangle list — so hg_upload_scene, the traversal and the CPU oracle take it unchanged.  Its images are
+// those of a different (valid) hierarchy, not the reference builder's: rays find the same nearest triangle except
+// where two lie within rounding of each other, and every traversal counter differs.  The GPU render of an SAH
+// hierarchy is still bit-exact against the oracle's render of the same hierarchy (tests/test_gpu_fast_bvh.py).
+// Boxes are their triangles' float min / max through the reference's Bounds arithmetic (padded when thin).
+// ---------------------------------------------------------------------------------------------------------------------
+namespace {
+
+struct Box3 {
+    float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
+                   std::numeric_limits<float>::infinity()};
+    float hi[3] = {-std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                   -std::numeric_limits<float>::infinity()};
+    void add(const float* p) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = p[k] < lo[k] ? p[k] : lo[k];
+            hi[k] = p[k] > hi[k] ? p[k] : hi[k];
+        }
+    }
+    void add(const Box3& b) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = b.lo[k] < lo[k] ? b.lo[k] : lo[k];
+            hi[k] = b.hi[k] > hi[k] ? b.hi[k] : hi[k];
+        }
+    }
+    double area() const {
+        if (!(hi[0] >= lo[0])) return 0.0;
+        const double dx = double(hi[0]) - lo[0], dy = double(hi[1]) - lo[1], dz = double(hi[2]) - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+constexpr int kSahBins = 32;
+
+}  // namespace
+
+extern "C" int64_t hg_build_blas_sah(const float* V, int32_t n_vertices, int32_t* idx, int32_t n_tris,
+                                     int32_t max_leaf, int32_t max_depth, BVHEntry* out_nodes, int64_t max_nodes) {
+    if (!V || !idx || n_tris < 0 || n_vertices < 0 || max_leaf < 1 || max_leaf > 15 || max_depth < 1) return HG_E_INVALID;
+    for (int64_t i = 0; i < 3 * int64_t(n_tris); ++i)
+        if (idx[i] < 0 || idx[i] >= n_vertices) return HG_E_INVALID;
+    const size_t n = size_t(n_tris);
+    std::vector<Box3> tb(n);
+    std::vector<float> cen(3 * n);
+    for (size_t t = 0; t < n; ++t) {
+        for (int v = 0; v < 3; ++v) tb[t].add(V + 3 * size_t(idx[3 * t + v]));
+        for (int k = 0; k < 3; ++k) cen[3 * t + k] = 0.5f * tb[t].lo[k] + 0.5f * tb[t].hi[k];
+    }
+    std::vector<uint32_t> ord(n);  // triangle order; idx is rewritten from it at the end
+    for (size_t t = 0; t < n; ++t) ord[t] = uint32_t(t);
+    std::vector<BVHEntry> nodes;
+    nodes.reserve(2 * n + 1);
+    // boxes through the reference's Bounds arithmetic (centre / extents round trip, and the AABBEpsilon pad of a box
+    // thinner than it on any axis, BVHGenerator.cs:154-186): a flat wall's leaves keep the thickness every traversal
+    // of the reference relies on
+    auto entry = [&](uint32_t first, uint32_t count, const Box3& b) {
+        UnityBounds u = UnityBounds::FromMinMax(Vec3{{b.lo[0], b.lo[1], b.lo[2]}}, Vec3{{b.hi[0], b.hi[1], b.hi[2]}});
+        u.PadIfThin();
+        return MakeEntry(u.Min(), u.Max(), first, count);
+    };
+    auto range_box = [&](uint32_t first, uint32_t count) {
+        Box3 b;
+        for (uint32_t i = first; i < first + count; ++i) b.add(tb[ord[i]]);
+        return b;
+    };
+    nodes.push_back(entry(0, uint32_t(n), range_box(0, uint32_t(n))));
+    if (n == 0) nodes[0].triangleCount = 0, nodes[0].indexA = 0;
+    struct Job {
+        uint32_t node, depth;
+    };
+    std::vector<Job> jobs{{0u, 0u}};
+    while (!jobs.empty()) {
+        const Job j = jobs.back();
+        jobs.pop_back();
+        const uint32_t first = nodes[j.node].indexA, count = nodes[j.node].triangleCount;
+        if (count <= uint32_t(max_leaf) || j.depth + 1 >= uint32_t(max_depth)) {
+            if (count > 15u && j.depth + 1 >= uint32_t(max_depth)) return HG_E_UNSUPPORTED;  // too deep to split
+            continue;
+        }
+        Box3 cb;  // centroid bounds
+        for (uint32_t i = first; i < first + count; ++i) cb.add(&cen[3 * size_t(ord[i])]);
+        int best_axis = -1;
+        uint32_t best_bin = 0;
+        double best_cost = std::numeric_limits<double>::infinity();
+        for (int ax = 0; ax < 3; ++ax) {
+            const float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.0f)) continue;
+            Box3 bins[kSahBins];
+            uint32_t cnt[kSahBins] = {};
+            const float scale = float(kSahBins) / ext;
+            for (uint32_t i = first; i < first + count; ++i) {
+                const uint32_t t = ord[i];
+                int b = int((cen[3 * size_t(t) + ax] - cb.lo[ax]) * scale);
+                b = b < 0 ? 0 : b >= kSahBins ? kSahBins - 1 : b;
+                bins[b].add(tb[t]);
+                cnt[b]++;
+            }
+            double right_area[kSahBins];
+            uint32_t right_cnt[kSahBins];
+            Box3 acc;
+            uint32_t c = 0;
+            for (int b = kSahBins - 1; b > 0; --b) {
+                acc.add(bins[b]);
+                c += cnt[b];
+                right_area[b] = acc.area();
+                right_cnt[b] = c;
+            }
+            Box3 left;
+            uint32_t lc = 0;
+            for (int b = 0; b < kSahBins - 1; ++b) {
+                left.add(bins[b]);
+                lc += cnt[b];
+                if (lc == 0 || right_cnt[b + 1] == 0) continue;
+                const double cost = left.area() * lc + right_area[b + 1] * right_cnt[b + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = ax;
+                    best_bin = uint32_t(b);
+                }
+            }
+        }
+        const double parent_area = nodes[j.node].triangleCount ? range_box(first, count).area() : 0.0;
+        // leaf if no split separates the centroids, or (small enough to be an inline leaf) splitting costs more than
+        // testing every triangle (traversal step ~ one triangle test)
+        uint32_t mid = first;
+        if (best_axis >= 0) {
+            const float ext = cb.hi[best_axis] - cb.lo[best_axis], scale = float(kSahBins) / ext;
+            uint32_t* lo = ord.data() + first;
+            uint32_t* hi = ord.data() + first + count;
+            while (lo < hi) {
+                int b = int((cen[3 * size_t(*lo) + best_axis] - cb.lo[best_axis]) * scale);
+                b = b < 0 ? 0 : b >= kSahBins ? kSahBins - 1 : b;
+                if (uint32_t(b) <= best_bin) ++lo;
+                else std::swap(*lo, *--hi);
+            }
+            mid = uint32_t(lo - ord.data());
+            if (count <= 15u && parent_area > 0.0 && 1.0 + best_cost / parent_area >= double(count)) continue;
+        }
+        if (mid == first || mid == first + count) {  // degenerate centroids: split the range in half
+            if (count <= 15u) continue;
+            mid = first + count / 2;
+        }
+        const uint32_t a = uint32_t(nodes.size());
+        nodes.push_back(entry(first, mid - first, range_box(first, mid - first)));
+        nodes.push_back(entry(mid, first + count - mid, range_box(mid, first + count - mid)));
+        nodes[j.node].indexA = a;
+        nodes[j.node].triangleCount = 0;
+        jobs.push_back({a + 1, j.depth + 1});
+        jobs.push_back({a, j.depth + 1});
+    }
+    std::vector<int32_t> re(3 * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int v = 0; v < 3; ++v) re[3 * i + v] = idx[3 * size_t(ord[i]) + v];
+    std::memcpy(idx, re.data(), re.size() * sizeof(int32_t));
+    const int64_t nn = int64_t(nodes.size());
+    if (out_nodes) {
+        if (nn > max_nodes) return -(nn + 1);
+        std::memcpy(out_nodes, nodes.data(), size_t(nn) * sizeof(BVHEntry));
+    }
+    return nn;
+}

@@ -114,7 +114,7 @@ EXPORTS = [
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
     "hg_readback", "hg_readback_begin", "hg_readback_end", "hg_readback_begin_format", "hg_readback_end_data",
     "hg_pack_display", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
-    "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_unity_bounds", "hg_pack_triangles",
+    "hg_set_option", "hg_selftest", "hg_build_blas", "hg_build_blas_mt", "hg_build_blas_sah", "hg_unity_bounds", "hg_pack_triangles",
     "hg_comm_unique_id", "hg_comm_init_rank", "hg_comm_init_all", "hg_comm_gather", "hg_comm_synchronize",
     "hg_comm_readback", "hg_comm_readback_begin", "hg_comm_readback_end", "hg_comm_set_timeout_ms", "hg_comm_transport", "hg_comm_last_error", "hg_comm_destroy",
     "hg_comm_assemble_host",
@@ -167,6 +167,7 @@ def lib() -> C.CDLL:
         "hg_selftest": (i64, [P, i32, C.POINTER(i64)]),
         "hg_build_blas": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64]),
         "hg_build_blas_mt": (i64, [P, i32, P, i32, f32p, f32p, i32, P, i64, i32]),
+        "hg_build_blas_sah": (i64, [P, i32, P, i32, i32, i32, P, i64]),
         "hg_unity_bounds": (None, [f32p, f32p, i32, f32p, f32p]),
         "hg_pack_triangles": (C.c_int, [P, P, i32, P, i32, P]),
         "hg_comm_unique_id": (C.c_int, [C.c_char_p]),

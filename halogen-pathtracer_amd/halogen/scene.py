@@ -77,6 +77,22 @@ def pack_material(m: HalogenMaterial, material_id: int) -> abi.PackedHalogenMate
     return p
 
 
+# BLAS builder of the meshes constructed from here on: "reference" (BVHGenerator.cs, the drop-in's parity path) or
+# "sah" (hg_build_blas_sah: a binned-SAH hierarchy in the same format, NOT the reference's images)
+BLAS_BUILDERS = ("reference", "sah")
+_blas_builder = "reference"
+SAH_MAX_LEAF = 2
+
+
+def set_blas_builder(name: str) -> str:
+    """Select the BLAS builder for meshes built afterwards; returns the previous one."""
+    global _blas_builder
+    if name not in BLAS_BUILDERS:
+        raise ValueError(f"unknown BLAS builder {name!r}")
+    prev, _blas_builder = _blas_builder, name
+    return prev
+
+
 class RayTracingMesh:
     """RayTracingMesh.cs: submesh-0 triangles, vertices and normals of a mesh + its transform + material.
 
@@ -95,6 +111,7 @@ class RayTracingMesh:
         self.transform = transform
         self.material = material if material is not None else HalogenMaterial.default()
         self.max_hierarchy_depth = int(max_hierarchy_depth)
+        self.blas_builder = _blas_builder
         self._cache()
 
     def _cache(self):
@@ -108,9 +125,13 @@ class RayTracingMesh:
         nodes = (abi.BVHEntry * cap)()
         # the parallel build returns the same nodes and triangle order (tests/test_bvh.py); 8 workers measured
         # best on the GPU box's host (tools/bench_build.py: 871k triangles 0.12 s -> 0.05 s)
-        n = L.hg_build_blas_mt(self.vertices.ctypes.data, len(self.vertices), self.triangles.ctypes.data, n_tris,
-                               mn.ctypes.data_as(fp), mx.ctypes.data_as(fp), self.max_hierarchy_depth,
-                               C.cast(nodes, C.c_void_p), cap, min(8, len(os.sched_getaffinity(0))))
+        if self.blas_builder == "sah":
+            n = L.hg_build_blas_sah(self.vertices.ctypes.data, len(self.vertices), self.triangles.ctypes.data, n_tris,
+                                    SAH_MAX_LEAF, 48, C.cast(nodes, C.c_void_p), cap)
+        else:
+            n = L.hg_build_blas_mt(self.vertices.ctypes.data, len(self.vertices), self.triangles.ctypes.data, n_tris,
+                                   mn.ctypes.data_as(fp), mx.ctypes.data_as(fp), self.max_hierarchy_depth,
+                                   C.cast(nodes, C.c_void_p), cap, min(8, len(os.sched_getaffinity(0))))
         if n < 0:
             raise abi.HalogenError(f"hg_build_blas failed for {self.name}: {n}")
         self.bvh = (abi.BVHEntry * n)()

@@ -419,6 +419,16 @@ int64_t hg_build_blas_mt(const float* vertices, int32_t n_vertices, int32_t* ind
                          const float root_min[3], const float root_max[3], int32_t max_hierarchy_depth,
                          BVHEntry* out_nodes, int64_t max_nodes, int32_t n_threads);
 
+/* Fast BLAS, NOT the reference's hierarchy (an SAH variant behind a non-parity choice): a
+ * binned surface-area-heuristic build into the same BVHEntry format (children of g at indexA, indexA + 1; leaves of at
+ * most max_leaf <= 15 triangles, ranges of the reordered `indices`; min/max boxes through the reference's Bounds
+ * arithmetic, padded when thin as BVHGenerator pads them; depth < max_depth).
+ * Any caller may pass its nodes to hg_upload_scene in place of hg_build_blas's: the render is then a different valid
+ * hierarchy's (the same nearest triangles except within rounding, other traversal counters).  Returns the node count,
+ * -(count + 1) if max_nodes is too small, or HG_E_INVALID / HG_E_UNSUPPORTED (the depth cap left a leaf over 15). */
+int64_t hg_build_blas_sah(const float* vertices, int32_t n_vertices, int32_t* indices, int32_t n_tris,
+                          int32_t max_leaf, int32_t max_depth, BVHEntry* out_nodes, int64_t max_nodes);
+
 /* Unity Bounds.SetMinMax(min,max) followed by .min/.max (centre/extents round trip) — the arithmetic
  * every bound in the reference goes through (BVHGenerator.cs:171-183, RayTracingMesh.cs:106-117). */
 void hg_unity_bounds(const float in_min[3], const float in_max[3], int32_t pad_if_thin,
