@@ -84,6 +84,8 @@ struct hg_ctx {
 
     // counters / timing
     DevBuf counters_dev;
+    DevBuf timeline;  // HG_WAVE_TIMELINE analysis builds: the queue waves' times of the last launches
+    uint64_t timeline_launches = 0;
     hg_counters counters{};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events, pending_trace;
 

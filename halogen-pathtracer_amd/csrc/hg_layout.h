@@ -199,6 +199,11 @@
 #ifndef HG_NODE_DEDUP
 #define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
 #endif
+#ifndef HG_WAVE_TIMELINE
+#define HG_WAVE_TIMELINE 0  // analysis builds: queue waves record their start / queue-dry / end times (tools/wave_timeline.py)
+#endif
+#define HG_TIMELINE_LAUNCHES 64  // ... for the last this many queue launches, at most HG_TIMELINE_WAVES waves each
+#define HG_TIMELINE_WAVES 8192
 #ifndef HG_COHERENCE_STATS
 #define HG_COHERENCE_STATS 0  // analysis builds: histogram of distinct node records per descent round (hg_device.h)
 #endif
@@ -290,6 +295,8 @@ struct HgKernelParams {
     // streaming launches without the queue and without a frame split: each wave traces wave_units consecutive units
     // of the cost order (1: one tile per wave), its lanes taking their items one after another (UnitItems)
     uint32_t wave_units;
+    // analysis builds (HG_WAVE_TIMELINE=1), queue launches: per wave (start, queue dry, end, items) in 100-MHz ticks
+    unsigned long long* __restrict__ timeline;
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane

@@ -1034,6 +1034,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         wave_lds_sync();
     }
 #endif
+#if HG_WAVE_TIMELINE
+    uint64_t tl_start = 0, tl_dry = 0;
+    if (kQueue && kp.timeline) tl_start = __builtin_amdgcn_s_memrealtime();
+#endif
     bool work = false;
     uint32_t px = 0u, py = 0u;
     Counters c{0, 0, 0, 0, 0, 0, 0, 0};
@@ -1081,6 +1085,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             if (lane == 0u) lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
             wave_lds_sync();
             dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
+#if HG_WAVE_TIMELINE
+            if (dry && kp.timeline) tl_dry = __builtin_amdgcn_s_memrealtime();
+#endif
             if (!work && !dry) {
                 work = true;
                 bounce = kFreshLane;
@@ -1282,6 +1289,15 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     }
     if constexpr (kQueue) record_tile_cost(lane);
     else items.record_cost(kp, lane);
+#if HG_WAVE_TIMELINE
+    if (kQueue && kp.timeline && lane == 0u && blockIdx.x < HG_TIMELINE_WAVES) {
+        unsigned long long* const w = kp.timeline + 4u * blockIdx.x;
+        w[0] = tl_start;
+        w[1] = tl_dry;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = lds_get(hg_next_item);
+    }
+#endif
     if constexpr (kQueue) {
         // The last wave out resets the queue heads for the next launch on this stream (no memset launch per queue
         // launch: a blit kernel waited for a CU that the other streams' persistent waves held).  A wave leaves only

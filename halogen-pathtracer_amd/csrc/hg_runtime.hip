@@ -557,7 +557,7 @@ void hg_destroy(hg_ctx* c) {
     for (hg_ctx::TraceLane& L : c->lanes)
         if (L.stream) (void)hipStreamSynchronize(L.stream);
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
-                      &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
+                      &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->timeline, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
                       &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
                       &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->pool})
         release(*b);
@@ -1200,6 +1200,19 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     const int64_t auto_wu = std::min<int64_t>(HG_WAVE_UNITS_MAX, tiles / (int64_t(HG_WAVE_UNITS_ROUNDS) * slots));
                     kc.wave_units = uint32_t(c->wave_units > 0 ? c->wave_units : std::max<int64_t>(1, auto_wu));
                 }
+                kc.timeline = nullptr;
+#if HG_WAVE_TIMELINE
+                if (kc.queue) {
+                    const size_t per = size_t(HG_TIMELINE_WAVES) * 4u * sizeof(unsigned long long);
+                    if (!c->timeline.p && ensure_quiet(c, c->timeline, per * HG_TIMELINE_LAUNCHES) == HG_OK)
+                        (void)hipMemset(c->timeline.p, 0, c->timeline.bytes);
+                    if (c->timeline.p) {
+                        kc.timeline = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->timeline.p) +
+                                                                          per * (c->timeline_launches++ % HG_TIMELINE_LAUNCHES));
+                        (void)hipMemsetAsync(kc.timeline, 0, per, L.stream);  // rows of waves this launch lacks
+                    }
+                }
+#endif
                 kc.tile_order = nullptr;
                 kc.tile_cost = ordered ? static_cast<unsigned long long*>(L.tile_cost.p) : nullptr;
                 // this stream's buffers are free once the blend of its previous chunk has read them
@@ -1622,6 +1635,19 @@ int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
     const int64_t r = hg_selftest_rcp_all(tested);
     if (r < 0) return fail(c, HG_E_HIP, "self-test failed to run");
     return r;
+}
+
+// Analysis builds (HG_WAVE_TIMELINE=1) only, not part of halogen_abi.h: the ring of the last HG_TIMELINE_LAUNCHES queue
+// launches' wave records (start, queue dry, end in 100-MHz ticks, items numbered), HG_TIMELINE_WAVES x 4 u64 each, and
+// how many queue launches wrote it.  tools/wave_timeline.py
+int64_t hg_debug_timeline(hg_ctx* c, void* dst, size_t bytes) {
+    if (!c) return HG_E_INVALID;
+    if (int rc = hg_ctx_flush(c)) return rc;
+    if (!c->timeline.p) return 0;
+    if (int rc = set_device(c)) return rc;
+    HG_HIP(c, hipDeviceSynchronize());
+    HG_HIP(c, hipMemcpy(dst, c->timeline.p, std::min(bytes, c->timeline.bytes), hipMemcpyDeviceToHost));
+    return int64_t(c->timeline_launches);
 }
 
 int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
