@@ -199,6 +199,9 @@
 #ifndef HG_NODE_DEDUP
 #define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
 #endif
+#ifndef HG_DRAIN_PRIO
+#define HG_DRAIN_PRIO 0  // A/B: streaming waves at priority 2 / 1 (traversal / shading), queue waves past the queue's end at 0
+#endif
 #ifndef HG_WAVE_TIMELINE
 #define HG_WAVE_TIMELINE 0  // analysis builds: queue waves record their start / queue-dry / end times (tools/wave_timeline.py)
 #endif

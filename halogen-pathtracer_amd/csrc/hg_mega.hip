@@ -1074,7 +1074,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         }
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
-#if HG_SHADE_PRIO >= 2
+#if HG_DRAIN_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#elif HG_SHADE_PRIO >= 2
     __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);  // traversal waits on memory: its waves issue first
 #endif
     for (;;) {
@@ -1109,7 +1111,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             cyc_trav += t;
             cyc_shade -= t;
         }
-#if HG_SHADE_PRIO == 1
+#if HG_DRAIN_PRIO  // (A/B) a queue wave past its queue's end drains at the lowest priority in both phases
+        if (kQueue && dry) __builtin_amdgcn_s_setprio(0);
+        else __builtin_amdgcn_s_setprio(1);
+#elif HG_SHADE_PRIO == 1
         __builtin_amdgcn_s_setprio(1);
 #elif HG_SHADE_PRIO >= 2
         __builtin_amdgcn_s_setprio(0);
@@ -1280,7 +1285,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             }
 #endif
         }
-#if HG_SHADE_PRIO == 1
+#if HG_DRAIN_PRIO
+        if (kQueue && dry) __builtin_amdgcn_s_setprio(0);
+        else __builtin_amdgcn_s_setprio(2);
+#elif HG_SHADE_PRIO == 1
         __builtin_amdgcn_s_setprio(0);
 #elif HG_SHADE_PRIO >= 2
         __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);
