@@ -64,6 +64,12 @@
 #ifndef HG_DESCENT_T
 #define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
 #endif
+#ifndef HG_STREAM_TMIN_DEEP
+#define HG_STREAM_TMIN_DEEP 20  // ... for a deep BLAS (C3 +0.6 %, C3F +1.0 %, strict 1-frame +1.5 %; C2 keeps 16: -1.2 %;
+#endif                          // tools/sweeps/sweep_r04_results.txt)
+#ifndef HG_STREAM_RESHADE_DEEP
+#define HG_STREAM_RESHADE_DEEP 24
+#endif
 #ifndef HG_STREAM_RESHADE
 #define HG_STREAM_RESHADE 16  // streaming kernel: repeat the shading pass while at least this many lanes need it
 #endif
@@ -306,6 +312,7 @@ struct HgKernelParams {
     uint32_t hot_records;  // HG_NODE_CACHE: node records [0, hot_records) are served from the wave's LDS copy
     uint32_t mesh_lds_word;  // HG_MESH_LDS: LDS word where the wave's copy of the mesh records starts
     uint32_t descent_t;    // relaxed while-while threshold (hg_device.h isect_meshes), 0 = classic while-while
+    uint32_t stream_deep;  // streaming kernel: the deep-BLAS shading thresholds (HG_STREAM_TMIN_DEEP / _RESHADE_DEEP)
     uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
     uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)
     uint32_t spill_stride;          // = threads of the launch grid

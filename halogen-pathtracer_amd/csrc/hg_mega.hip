@@ -988,8 +988,12 @@ __device__ __forceinline__ float bpermf(uint32_t src, float v) { return __uint_a
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
 // Every frame's colour goes to frame_color (item scheduling), blended in frame order by hg_blend_frames.  kQueue: the
 // persistent work-queue form above (launches of few frames).
-template <bool kCounters, bool kMeshLds, bool kQueue>
+template <bool kCounters, bool kMeshLds, bool kQueue, bool kDeep>
 __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
+    // shade once at most kTmin lanes still traverse; reshade while at least kReshade need it (compile-time: as kernel
+    // parameters they cost 8 B of scratch)
+    constexpr uint32_t kTmin = kDeep ? HG_STREAM_TMIN_DEEP : HG_STREAM_TMIN;
+    constexpr uint32_t kReshade = kDeep ? HG_STREAM_RESHADE_DEEP : HG_STREAM_RESHADE;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
     const uint32_t n_units = nlt * split;  // kQueue: (tile, frame chunk) units of the queue
@@ -1103,7 +1107,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             const bool act = work && tv.mi < nm;
             const uint64_t am = wave_ballot(act);
             // (work includes act: some lane waits to shade iff the work mask differs)
-            if (am == 0ull || (uint32_t(__builtin_popcountll(am)) <= HG_STREAM_TMIN && wave_ballot(work) != am)) break;
+            if (am == 0ull || (uint32_t(__builtin_popcountll(am)) <= kTmin && wave_ballot(work) != am)) break;
             trav_step<kMeshLds>(kp, ray, tv, c, stk, act, ls);
         }
         if (kCounters) {
@@ -1124,7 +1128,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
         for (uint32_t it = 0;; ++it) {
             const uint32_t n_sh = wave_count(work && tv.mi >= nm);
-            if (n_sh == 0u || (it > 0u && n_sh < HG_STREAM_RESHADE)) break;
+            if (n_sh == 0u || (it > 0u && n_sh < kReshade)) break;
 #if HG_RAY_SORT
             bool began = false;  // this lane begins a ray (its traversal starts after the sort below)
 #endif
@@ -1355,17 +1359,24 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
     const dim3 g{uint32_t(grid)}, b{64u};
     const size_t sh = mesh_lds ? mesh_lds : lds;
+    // deep BLAS (kp.stream_deep): the kDeep thresholds
+#define HG_STREAM_LAUNCH(C, M, Q)                                                                                      \
+    do {                                                                                                               \
+        if (kp.stream_deep) hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, true>), g, b, sh, stream, kp);        \
+        else hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, false>), g, b, sh, stream, kp);                      \
+    } while (0)
     if (queue) {
-        if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true, true>), g, b, sh, stream, kp);
-        else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false, true>), g, b, sh, stream, kp);
-        else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true, true>), g, b, sh, stream, kp);
-        else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false, true>), g, b, sh, stream, kp);
+        if (counters && mesh_lds) HG_STREAM_LAUNCH(true, true, true);
+        else if (counters) HG_STREAM_LAUNCH(true, false, true);
+        else if (mesh_lds) HG_STREAM_LAUNCH(false, true, true);
+        else HG_STREAM_LAUNCH(false, false, true);
     } else {
-        if (counters && mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<true, true, false>), g, b, sh, stream, kp);
-        else if (counters) hipLaunchKernelGGL((hg_trace_stream_kernel<true, false, false>), g, b, sh, stream, kp);
-        else if (mesh_lds) hipLaunchKernelGGL((hg_trace_stream_kernel<false, true, false>), g, b, sh, stream, kp);
-        else hipLaunchKernelGGL((hg_trace_stream_kernel<false, false, false>), g, b, sh, stream, kp);
+        if (counters && mesh_lds) HG_STREAM_LAUNCH(true, true, false);
+        else if (counters) HG_STREAM_LAUNCH(true, false, false);
+        else if (mesh_lds) HG_STREAM_LAUNCH(false, true, false);
+        else HG_STREAM_LAUNCH(false, false, false);
     }
+#undef HG_STREAM_LAUNCH
     return hipGetLastError();
 }
 

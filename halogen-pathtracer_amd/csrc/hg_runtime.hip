@@ -1040,6 +1040,7 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                                                      : c->kernel;
     const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     // relaxed descent threshold: 3 for the regen / lockstep kernels, HG_STREAM_DESCENT_T for the streaming one
+    kp.stream_deep = deep_blas ? 1u : 0u;
     kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
                    : !deep_blas      ? 0u
                    : kern == HG_KERNEL_MEGA_STREAM ? uint32_t(HG_STREAM_DESCENT_T)
