@@ -184,6 +184,18 @@ struct Mat {
     float4 albedo, spec_metal, emis_rough, absorb_ior, prio_id_r2;
 };
 __device__ __forceinline__ Mat load_mat(const HgKernelParams& kp, uint32_t m) {
+#if HG_MAT_SCALAR
+    // every active lane shading the same material (one glass, one wall): five scalar loads through the constant
+    // cache instead of five vector-memory instructions on the texture-data unit that binds the kernel
+    const uint32_t m0 = uint32_t(__builtin_amdgcn_readfirstlane(int(m)));
+    if (__builtin_amdgcn_ballot_w64(m != m0) == 0ull) {
+        typedef const __attribute__((address_space(4))) float* cfp;
+        const cfp q = (cfp)(uintptr_t)(kp.materials + 5u * m0);
+        return Mat{make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]),
+                   make_float4(q[8], q[9], q[10], q[11]), make_float4(q[12], q[13], q[14], q[15]),
+                   make_float4(q[16], q[17], q[18], q[19])};
+    }
+#endif
     const float4* p = kp.materials + 5 * m;
     return Mat{p[0], p[1], p[2], p[3], p[4]};
 }

@@ -205,6 +205,9 @@
 #ifndef HG_NODE_DEDUP
 #define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
 #endif
+#ifndef HG_MAT_SCALAR
+#define HG_MAT_SCALAR 0  // A/B: a material record the wave's shading lanes share is read with scalar loads
+#endif
 #ifndef HG_DRAIN_PRIO
 #define HG_DRAIN_PRIO 0  // A/B: streaming waves at priority 2 / 1 (traversal / shading), queue waves past the queue's end at 0
 #endif
