@@ -89,3 +89,22 @@ def test_gpu_fuzz_matches_oracle(gpu, seed, kernel):
     assert_bitwise(img, ref, f"fuzz seed {seed}, kernel {kernel}")
     for k in ("rays", "tri_tests", "aabb_tests", "hits"):
         assert cnt[k] == rcnt[k], (k, cnt[k], rcnt[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS[:12])
+def test_gpu_fuzz_sah_tree_matches_oracle(gpu, seed):
+    """The same random scenes with every mesh's hierarchy from hg_build_blas_sah (not the reference builder's):
+    the kernel traverses any tree the reference's way, so it still equals the oracle on the same tree, bit for bit."""
+    from halogen import scene as sc
+
+    prev = sc.set_blas_builder("sah")
+    try:
+        packed, params, frames, acc, cube = _case(seed)
+    finally:
+        sc.set_blas_builder(prev)
+    img, cnt = gpu_render(packed, params, frames, acc, cube=cube)
+    ref, rcnt = hg_oracle.render(packed, params, frames, acc, cubemap=cube)
+    assert_bitwise(img, ref, f"fuzz seed {seed} on SAH trees")
+    for k in ("rays", "tri_tests", "aabb_tests", "hits"):
+        assert cnt[k] == rcnt[k], (k, cnt[k], rcnt[k])
