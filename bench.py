@@ -721,30 +721,59 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    local = None
-    if dist is not None and comm is None:  # the torch gather's staging tensor and rank 0's pixel index, set up untimed
-        import torch
+    gather_error = None
+    for attempt in range(2):
+        local = None
+        if dist is not None and comm is None:  # the torch gather's staging tensor and rank 0's pixel index, untimed
+            import torch
 
-        from halogen import distributed as hd
+            from halogen import distributed as hd
 
-        local = torch.empty((ctx.local_tile_count(), 64, 4), dtype=torch.float32, device=f"cuda:{device}")
-        if rank == 0:
-            tx, ty = hd.tiles_xy(W, H)
-            hd.pixel_index(world, hd.local_tile_count(tx * ty, 0, world), W, H, torch.device(coll_dev))
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.render(frames_per_step, True)
-    gathered = None
-    if comm is not None:
-        comm.gather(0)  # enqueued on the context stream after the renders
-        comm.synchronize()  # bounded wait (deadline + RCCL async errors) before the barrier's unbounded one
-    elif dist is not None:
-        ctx.copy_tiles_device(local.data_ptr(), local.numel() * 4)
-        # assembled on rank 0's device (as the N=1 image stays in the accumulator); to the host after the clock
-        gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H, on_device=True)
-    barrier()
-    dt = time.perf_counter() - t0
+            local = torch.empty((ctx.local_tile_count(), 64, 4), dtype=torch.float32, device=f"cuda:{device}")
+            if rank == 0:
+                tx, ty = hd.tiles_xy(W, H)
+                hd.pixel_index(world, hd.local_tile_count(tx * ty, 0, world), W, H, torch.device(coll_dev))
+        if attempt:  # the rerun after a failed hg_comm gather starts from a cleared accumulator again
+            ctx.clear_accumulation()
+            ctx.set_params(params)
+            ctx.reset_counters()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.render(frames_per_step, True)
+        gathered = None
+        failed = None
+        if comm is not None:
+            try:
+                comm.gather(0)  # enqueued on the context stream after the renders
+                comm.synchronize()  # bounded wait (deadline + RCCL async errors) before the barrier's unbounded one
+            except abi.HalogenError as e:
+                failed = f"rank {rank}: {str(e)[:300]}"
+        elif dist is not None:
+            ctx.copy_tiles_device(local.data_ptr(), local.numel() * 4)
+            # assembled on rank 0's device (as the N=1 image stays in the accumulator); to the host after the clock
+            gathered = hd.gather_tiles(local.to(coll_dev), rank, world, W, H, on_device=True)
+        barrier()
+        dt = time.perf_counter() - t0
+        if comm is not None:
+            # after the clock: if any rank's hg_comm gather failed, every rank reruns the timed region with the torch
+            # gather and the line says why (`gather_error`), so a broken transport never costs the measurement
+            import torch
+
+            bad = torch.tensor([1 if failed else 0], dtype=torch.int32, device=coll_dev)
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+            if int(bad.item()) and attempt == 0:
+                errs = [None] * world
+                dist.all_gather_object(errs, failed)
+                gather_error = "; ".join(e for e in errs if e) or "a peer's gather failed"
+                try:
+                    comm.close()
+                except abi.HalogenError:
+                    pass
+                comm = None
+                gather_mode = "torch"
+                continue
+        break
     if comm is not None and rank == 0:
         gathered = comm.readback(W, H)
     elif gathered is not None:
@@ -752,7 +781,7 @@ def main():
 
     abi_check = None
     gather_ms = {}
-    if dist is not None and not args.no_abi_check and comm_init_error is None:
+    if dist is not None and not args.no_abi_check and comm_init_error is None and gather_error is None:
         import torch
 
         from halogen import distributed as hd
@@ -893,6 +922,7 @@ def main():
             if dist is not None else None,
             "abi_gather_check": abi_check,
             "gather_init_error": comm_init_error,
+            "gather_error": gather_error,
             # each gather alone (after the timed region; max over ranks): the one `gather` names is inside `value`
             "gather_ms": gather_ms or None,
             "setup_s": setup_s,
