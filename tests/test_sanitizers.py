@@ -22,6 +22,7 @@ from halogen import host_files
 ROOT = Path(__file__).resolve().parents[1]
 ASAN = ROOT / "oracle" / "build" / "hg_oracle_asan"
 TSAN = ROOT / "halogen-pathtracer_amd" / "build" / "tsan_blas"
+ASAN_SAH = ROOT / "halogen-pathtracer_amd" / "build" / "asan_sah"
 ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
            UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1:exitcode=66")
 
@@ -96,3 +97,11 @@ def test_host_pool_under_tsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-2000:]
     assert r.stdout.split()[0] == str(500 * 1000)
+
+
+def test_sah_builder_under_asan_ubsan():
+    """hg_build_blas_sah (the non-reference SAH hierarchy, csrc/hg_host.cpp) under AddressSanitizer + UBSan: random
+    soups, a flat grid (every box thin, padded), coincident triangles, an empty mesh; every triangle in one leaf."""
+    subprocess.run(["make", "-s", "-C", str(ROOT / "halogen-pathtracer_amd"), "asan_sah"], check=True)
+    out = run([ASAN_SAH, 20000, 7])
+    assert out.count("every triangle in one leaf") == 10, out
