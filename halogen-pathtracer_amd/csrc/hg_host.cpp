@@ -675,7 +675,7 @@ extern "C" int64_t hg_build_blas_sah(const float* V, int32_t n_vertices, int32_t
     std::vector<int32_t> re(3 * n);
     for (size_t i = 0; i < n; ++i)
         for (int v = 0; v < 3; ++v) re[3 * i + v] = idx[3 * size_t(ord[i]) + v];
-    std::memcpy(idx, re.data(), re.size() * sizeof(int32_t));
+    if (!re.empty()) std::memcpy(idx, re.data(), re.size() * sizeof(int32_t));
     const int64_t nn = int64_t(nodes.size());
     if (out_nodes) {
         if (nn > max_nodes) return -(nn + 1);
