@@ -67,3 +67,27 @@ def test_roofline_prices_the_binding_unit(bench, monkeypatch):
     del pmc["vmem_insts_per_launch"]
     r = bench.roofline_of(pmc, 0.0384, 625e9, "hg_trace_stream_kernel")
     assert r["bound"] == "valu" and r["frac"] == pytest.approx(26.92 / 0.0384 / 1228.8)
+
+
+def test_committed_bench_line_keeps_the_contract():
+    """The round's committed bench line (profiles/r04y_bench.json, the shipped library on the GPU box) carries the
+    driver's contract keys, the roofline priced on the vector-memory unit from the committed profile of the same
+    library, the cpu_baseline, and the second numbers beside the headline (framed, per_frame, fast_bvh)."""
+    import json
+
+    line = json.loads((ROOT / "profiles" / "r04y_bench.json").read_text().strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["unit"] == "Mpaths/s" and line["n_gpus"] == 1 and line["higher_is_better"] is True
+    assert line["config"]["workload"].startswith("C3") and line["config"]["frames_per_step"] == 64
+    r = line["roofline"]
+    assert r["bound"] == "vmem" and r["counters_library_matches"] is True
+    assert r["counters_from"] == "profiles/r04y_C3_summary.json" and (ROOT / r["counters_from"]).exists()
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and 0.3 < r["frac"] < 1.0
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
+    assert line["counting_replay_bit_identical"] is True
+    assert line["per_frame"]["bit_identical_to_batched"] == {"coalesce_1": True, "coalesce_32": True}
+    fast = line["fast_bvh"]
+    assert fast["value"] > line["value"] and fast["pixels_differing_from_headline_image"] < 1e-3
