@@ -552,6 +552,7 @@ def main():
     ap.add_argument("--tile-order", type=int, default=-1, help="HG_OPT_TILE_ORDER (0 off, 1 on); -1: default")
     ap.add_argument("--wave-units", type=int, default=-1, help="HG_OPT_WAVE_UNITS (0 auto, k tiles per wave); -1: default")
     ap.add_argument("--lane-pick", type=int, default=-1, help="HG_OPT_LANE_PICK (0 in turn, 1 first idle); -1: default")
+    ap.add_argument("--readback-stream", type=int, default=0, help="--per-frame-only: HG_OPT_READBACK_STREAM (1 side)")
     ap.add_argument("--bvh", default="reference", choices=["reference", "sah"],
                     help="BLAS builder of the timed scene: the reference's (the drop-in's parity path, the contract line) "
                          "or hg_build_blas_sah (NOT the reference's hierarchy; A/B and the fast_bvh leg)")
@@ -667,6 +668,7 @@ def main():
         ctx.set_option(abi.HG_OPT_COALESCE, args.coalesce)
         depth = 1 if args.display == "sync" else args.readback_depth
         ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+        ctx.set_option(abi.HG_OPT_READBACK_STREAM, args.readback_stream)
         fmt = abi.DISPLAY_FORMATS[args.display_format]
         for _ in range(frames_per_step // args.launch_frames):  # warm-up step of the timed launches (their buffers)
             ctx.render(args.launch_frames, True)

@@ -205,6 +205,9 @@
 #ifndef HG_NODE_DEDUP
 #define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
 #endif
+#ifndef HG_RB_OWN_QUEUE
+#define HG_RB_OWN_QUEUE 1  // HG_OPT_READBACK_STREAM's copy stream CU-masked, on a hardware queue of its own: a plain one shares
+#endif                     // a queue with a trace lane and waits behind its traces (depth 2: 1,285 -> 1,642; sweep_r04_rbq)
 #ifndef HG_MAT_SCALAR
 #define HG_MAT_SCALAR 0  // A/B: a material record the wave's shading lanes share is read with scalar loads
 #endif

@@ -1390,7 +1390,11 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
     // frames' blends) does not wait for the copy; else c->image, copied on the context stream
     const bool side = c->rb_side != 0;
     if (side && !c->rb_stream) {
+#if HG_RB_OWN_QUEUE  // the copy stream on a hardware queue of its own (a plain stream shares one with a trace lane)
+        HG_HIP(c, create_lane_stream(c, HG_TRACE_LANES, &c->rb_stream));
+#else
         HG_HIP(c, hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking));
+#endif
         for (int j = 0; j < HG_READBACK_MAX; ++j)
             HG_HIP(c, hipEventCreateWithFlags(&c->rb_untiled[j], hipEventDisableTiming));
     }
