@@ -131,11 +131,13 @@ def fast_bvh_measurement(ctx, cfg, packed, cube, params, W, H, frames_per_step: 
     ctx.clear_accumulation()
     ctx.set_params(params)
     ctx.synchronize()
+    ctx.reset_counters()
     t0 = time.perf_counter()
     for _ in range(steps):
         ctx.render(frames_per_step, True)
     ctx.synchronize()
     dt = time.perf_counter() - t0
+    timing = ctx.counters()  # trace-kernel launch durations (HIP events on the trace streams)
     img = ctx.readback(W, H)
     differ = (img.view(np.uint32) != ref_img.view(np.uint32)).any(-1)
     d = np.abs(img.astype(np.float64) - ref_img.astype(np.float64))
@@ -148,7 +150,13 @@ def fast_bvh_measurement(ctx, cfg, packed, cube, params, W, H, frames_per_step: 
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)
     ctx.upload_scene(packed)  # the reference tree again for the legs after this one
     value = W * H * frames_per_step * steps / dt / 1e6
+    kernel_symbol = KERNEL_SYMBOL.get(int(c["last_kernel"]), "?")
+    mean_launch_s, span_s = launch_seconds(timing)
+    # its own roofline, from the committed PMC pass of this workload (profiles/pmc_traffic_C3SAH.json)
+    roofline = roofline_of(committed_counters("C3SAH", W, H, frames_per_step, kernel_symbol), mean_launch_s,
+                           algorithmic_bytes(c), kernel_symbol, dt / steps, span_s)
     return {"workload": "C3 on an SAH BLAS (hg_build_blas_sah, max leaf 2): not the reference's hierarchy",
+            "roofline": roofline,
             "value": value, "unit": "Mpaths/s", "steps": steps, "ms_per_step": dt * 1e3 / steps,
             "frac_of_headline": value / headline, "build_s": build_s, "blas_nodes": len(sah.blas),
             "pixels_differing_from_headline_image": float(differ.mean()),

@@ -9,7 +9,7 @@ OUT=$PWD/gpurun_out/prof
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for cfg in $CONFIGS; do
-  ARGS="--config $cfg --steps ${STEPS:-8} --warmup 2 --no-cpu-baseline --no-framed --no-per-frame --no-counters"
+  ARGS="--config $cfg --steps ${STEPS:-8} --warmup 2 --no-cpu-baseline --no-framed --no-per-frame --no-counters ${BENCH_EXTRA:-}"
   run() {  # name, extra rocprofv3 args...
     local name=$1; shift
     timeout -k 10 240 rocprofv3 "$@" -d "$OUT/${TAG}_${cfg}_${name}" -o "$name" --output-format csv -- \
