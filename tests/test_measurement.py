@@ -91,3 +91,6 @@ def test_committed_bench_line_keeps_the_contract():
     assert line["per_frame"]["bit_identical_to_batched"] == {"coalesce_1": True, "coalesce_32": True}
     fast = line["fast_bvh"]
     assert fast["value"] > line["value"] and fast["pixels_differing_from_headline_image"] < 1e-3
+    fr = fast["roofline"]
+    assert fr["bound"] == "vmem" and fr["counters_library_matches"] is True
+    assert fr["counters_from"] == "profiles/r04x_sah_C3_summary.json" and (ROOT / fr["counters_from"]).exists()
