@@ -238,7 +238,29 @@
 // The queue of a kQueue launch: 8 unit heads, 128 B apart (words 32 h), then the count of waves that have left (its own
 // 128-B line): the last wave out zeroes them for the next launch (the runtime zeroes the buffer once, at allocation)
 #define HG_QUEUE_DONE_WORD 256u
+#ifndef HG_PATH_MIGRATE
+#define HG_PATH_MIGRATE 0  // kQueue drain: waves left with few paths hand them to other waves at ray boundaries (§4.6)
+#endif
+#ifndef HG_MIG_KERNEL
+#define HG_MIG_KERNEL HG_PATH_MIGRATE  // (A/B: 0 keeps the runtime side only)
+#endif
+#ifndef HG_MIG_RETIRE
+#define HG_MIG_RETIRE 16  // ... a queue-dry wave with at most this many paths in flight retires (exports, then leaves)
+#endif
+#ifndef HG_MIG_POLL_IDLE
+#define HG_MIG_POLL_IDLE 16  // ... a dry wave tests the pool (a device-coherent load) with at least this many idle lanes
+#endif
+#ifndef HG_MIG_KEEP_SHIFT
+#define HG_MIG_KEEP_SHIFT 1  // ... while at least gridDim >> this many of the launch's waves stay (all retiring: 3x slower)
+#endif
+// Path migration words of the queue buffer (each on its own 128-B line): the 64-bit (waves gone | exporting waves
+// << 32) state, the pool's (reserved | taken << 32) counts; then the pool, one 128-B record per exported path
+// (at most 64 per wave of the launch)
+#define HG_MIG_STATE_WORD 288u
+#define HG_MIG_POOL_WORD 320u
+#define HG_MIG_POOL_BYTE 2048u
 #define HG_QUEUE_BYTES (9u * 128u)
+#define HG_QUEUE_BYTES_MIG(slots) (size_t(HG_MIG_POOL_BYTE) + size_t(slots) * 64u * 128u)
 #ifndef HG_ITEMS_PIXEL_MAJOR
 #define HG_ITEMS_PIXEL_MAJOR 1  // items k -> (pixel k / frames, frame k % frames): a wave's lanes trace one pixel's frames
                                 // (with HG_FC_SLOT_MAJOR: C3 +0.4 %, C2 +0.5 %, C5 -0.4 %; tools/sweeps/sweep_r02_be/bf)

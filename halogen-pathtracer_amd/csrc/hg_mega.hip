@@ -953,6 +953,90 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
     y = ty * HG_TILE + ((slot >> 3) & 7u);
 }
 
+#if HG_MIG_KERNEL
+// Path migration (kQueue).  After the queue runs dry each wave drains: its lanes finish the paths they
+// hold, the idle ones waiting, the wave's slot held until its slowest path ends.  Here a dry wave with at most
+// HG_MIG_RETIRE paths left retires: each of its lanes, when its current ray ends and the path goes on, writes the
+// path's whole state (a ray boundary: no traversal state) to a pool record instead of beginning the ray, and the wave
+// leaves once its lanes are empty; the dry waves that stay take pool records into their idle lanes at the loop top.
+// A path's result does not depend on which lane traces it (the state moves bit for bit).  The 64-bit state word counts
+// the waves gone (retired or left) and, above bit 32, the retired waves still exporting: a wave retires only while
+// another wave of the launch is not gone, and the last one leaves only with no exporter left and the pool empty, so
+// every record is taken.  Records carry slot + 1 as their ready flag (0: not written yet), cleared by the taker.
+__device__ __forceinline__ uint32_t mig_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Device-coherent single words (relaxed agent-scope atomics: written through to / read from the coherent level).  No
+// acquire / release fences: at agent scope on gfx950 those write back or invalidate the XCD's whole L2, and one per
+// wave leaving made 1-frame launches 2x slower (the waves lost their cached nodes); mig_drain orders a lane's stores.
+__device__ __forceinline__ void mig_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mig_drain() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ unsigned long long* mig_state(const HgKernelParams& kp) {
+    return reinterpret_cast<unsigned long long*>(kp.queue + HG_MIG_STATE_WORD);
+}
+__device__ __forceinline__ uint4* mig_rec(const HgKernelParams& kp, uint32_t i) {
+    return reinterpret_cast<uint4*>(reinterpret_cast<char*>(kp.queue) + HG_MIG_POOL_BYTE) + 8u * i;
+}
+// the pool's counts in one 64-bit word: records reserved (low half) and taken (high half), one load to test it
+__device__ __forceinline__ unsigned long long* mig_pool(const HgKernelParams& kp) {
+    return reinterpret_cast<unsigned long long*>(kp.queue + HG_MIG_POOL_WORD);
+}
+__device__ __forceinline__ bool mig_pool_empty(const HgKernelParams& kp) {
+    const unsigned long long v = __hip_atomic_load(mig_pool(kp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return uint32_t(v >> 32) >= uint32_t(v);
+}
+// lane 0: retire the wave, unless the pool holds records to take or it would leave fewer than gridDim >> HG_MIG_KEEP_SHIFT
+// waves of the launch not gone (at least one)
+__device__ __forceinline__ bool mig_try_retire(const HgKernelParams& kp) {
+    if (!mig_pool_empty(kp)) return false;
+    unsigned long long* const s = mig_state(kp);
+    unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t = 0; t < 16; ++t) {
+        if (uint32_t(v) + 1u + (gridDim.x >> HG_MIG_KEEP_SHIFT) > gridDim.x || uint32_t(v) + 1u >= gridDim.x) return false;
+        if (__hip_atomic_compare_exchange_strong(s, &v, v + 1ull + (1ull << 32), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return true;
+    }
+    return false;
+}
+// lane 0 of a wave with no path: leave, if the pool is empty and either another wave is not gone or no retired wave
+// is still exporting (a successful exchange of the word read proves no wave retired since)
+__device__ __forceinline__ bool mig_try_leave(const HgKernelParams& kp) {
+    unsigned long long* const s = mig_state(kp);
+    unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t = 0; t < 16; ++t) {
+        if (uint32_t(v) + 1u >= gridDim.x && (v >> 32) != 0ull) return false;
+        if (!mig_pool_empty(kp)) return false;
+        if (__hip_atomic_compare_exchange_strong(s, &v, v + 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return true;
+    }
+    return false;
+}
+// lane 0: claim up to `want` pool records (first in `first`)
+__device__ __forceinline__ uint32_t mig_claim(const HgKernelParams& kp, uint32_t want, uint32_t& first) {
+    unsigned long long* const pool = mig_pool(kp);
+    unsigned long long v = __hip_atomic_load(pool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t p = uint32_t(v), q = uint32_t(v >> 32);
+        if (q >= p) return 0u;
+        const uint32_t n = min(want, p - q);
+        if (__hip_atomic_compare_exchange_strong(pool, &v, v + (uint64_t(n) << 32), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            first = q;
+            return n;
+        }
+    }
+    return 0u;
+}
+#endif
+
 #ifndef HG_RAY_SORT
 #define HG_RAY_SORT 0  // A/B (DESIGN.md §10 lever 7): 1 = sort the lanes beginning a ray by direction octant, 2 = by
                        // octant and dominant axis (24 keys), before their traversal
@@ -1056,6 +1140,12 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     tv.mi = nm;
     uint32_t slot = 0;  // the lane's item: kQueue its accumulator slot (local tile * 64 + pixel), else v (UnitItems)
     bool dry = false;   // kQueue, wave-uniform: the queue has no unit left
+#if HG_MIG_KERNEL
+    // (kQueue, wave-uniform) 1: the wave exports its paths at their ray boundaries, then leaves.  The kernel is at
+    // its scalar-register limit: every wave-uniform value live across the loop spills (a lane holding an imported
+    // path is marked by its mesh cursor, tv.mi = nm + 1, not by a mask)
+    uint32_t retiring = 0;
+#endif
     const UnitItems items = kQueue ? UnitItems() : UnitItems(kp, u_first, local_tile, chunk < split, f_begin, f_end, lane);
     if constexpr (kQueue) {
         wave_lds_sync();  // hg_q / hg_next_item initialised (lane 0); every lane takes its first item in the loop
@@ -1100,6 +1190,75 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 tv.mi = nm;
             }
         }
+#if HG_MIG_KERNEL
+        if (kQueue && dry) {  // (the whole wave converged)
+            if (retiring) {
+                if (!__any(work)) {  // every path exported or finished
+                    mig_drain();  // (the wave's records are flagged before it stops counting as exporting)
+                    if (lane == 0u)
+                        __hip_atomic_fetch_add(mig_state(kp), 0xFFFFFFFF00000000ull, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            } else {
+                // idle lanes take exported paths (their state as the exporting lane left it at a ray boundary)
+                // (each test of the pool is a device-coherent load, microseconds: a wave with most lanes busy tests it
+                // every HG_MIG_POLL-th loop only)
+                bool leave_now = false, poll = false;
+                uint32_t mig_spins = 0;
+                for (;;) {  // (an inner loop: a second latch of the outer loop cost the kernel scratch)
+                const uint64_t idle = wave_ballot(!work);
+                const uint32_t n_idle = uint32_t(__builtin_popcountll(idle));
+                poll = n_idle >= uint32_t(HG_MIG_POLL_IDLE);
+                uint32_t n = 0, q0 = 0;
+                if (poll && lane == 0u) n = mig_claim(kp, n_idle, q0);
+                n = __builtin_amdgcn_readfirstlane(n);
+                q0 = __builtin_amdgcn_readfirstlane(q0);
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
+                if (!work && r < n) {
+                    uint4* const rec = mig_rec(kp, q0 + r);
+                    uint32_t* const flag = &rec[6].x;
+                    uint32_t s1 = mig_ld(flag);
+                    for (uint32_t k = 0; s1 == 0u && k < (1u << 22); ++k) {  // (reserved: its writer is resident)
+                        __builtin_amdgcn_s_sleep(1);
+                        s1 = mig_ld(flag);
+                    }
+                    const uint32_t* const w = reinterpret_cast<const uint32_t*>(rec);
+                    ray.o = mk(__uint_as_float(mig_ld(w + 0)), __uint_as_float(mig_ld(w + 1)), __uint_as_float(mig_ld(w + 2)));
+                    ray.d = mk(__uint_as_float(mig_ld(w + 3)), __uint_as_float(mig_ld(w + 4)), __uint_as_float(mig_ld(w + 5)));
+                    s_thr.set(mk(__uint_as_float(mig_ld(w + 6)), __uint_as_float(mig_ld(w + 7)), __uint_as_float(mig_ld(w + 8))));
+                    s_col.set(mk(__uint_as_float(mig_ld(w + 9)), __uint_as_float(mig_ld(w + 10)), __uint_as_float(mig_ld(w + 11))));
+                    acc_rough = __uint_as_float(mig_ld(w + 12));
+                    fs = mig_ld(w + 13);
+                    bounce = mig_ld(w + 14);
+                    smp.frame = mig_ld(w + 15);
+                    smp.pixel = mig_ld(w + 16);
+                    smp.offset = mig_ld(w + 17);
+                    ms.s = uint64_t(mig_ld(w + 18)) | (uint64_t(mig_ld(w + 19)) << 32);
+                    ms.sp = int(mig_ld(w + 20));
+                    __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    slot = s1 - 1u;
+                    work = true;
+                    tv.mi = nm + 1u;  // waits to shade: the shading pass begins its ray
+                }
+                if (__any(work)) break;
+                uint32_t leave = 0;
+                if (lane == 0u) leave = mig_try_leave(kp) ? 1u : 0u;
+                if (__builtin_amdgcn_readfirstlane(leave) || ++mig_spins >= (1u << 22)) {
+                    leave_now = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);  // the launch's last wave: exporters are still at work
+                }
+                if (leave_now) break;
+                if (poll && kp.spp == 1 && wave_count(work) <= uint32_t(HG_MIG_RETIRE)) {  // (a sample sum stays)
+                    uint32_t ret = 0;
+                    if (lane == 0u) ret = mig_try_retire(kp) ? 1u : 0u;
+                    retiring = __builtin_amdgcn_readfirstlane(ret);
+                }
+            }
+        }
+#endif
         if (!__any(work)) break;
         // ---- traversal rounds until few lanes are left traversing
         if (kCounters) cyc_trav -= wave_clock();
@@ -1138,9 +1297,14 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             uint64_t tp = kCounters ? wave_clock() : 0;
 #endif
             const bool fresh = kQueue && bounce == kFreshLane;  // no path yet: straight to the take below
-            bool alive = false;
+#if HG_MIG_KERNEL
+            const bool imported = kQueue && tv.mi == nm + 1u;  // begin the imported path's ray
+#else
+            constexpr bool imported = false;
+#endif
+            bool alive = imported;
             f3 thr = s_thr.get(), col = s_col.get();
-            if (!fresh) {
+            if (!fresh && !imported) {
             const Hit hit = trav_hit<kMeshLds>(kp, ray, tv);
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 11, tp);
@@ -1236,6 +1400,28 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
 #if HG_PHASE_DETAIL == 1
             if (kCounters) tp = phase_mark(kp, 13, tp);
 #endif
+#if HG_MIG_KERNEL
+            if (kQueue && retiring && alive) {  // export the path at its ray boundary (taken by a staying wave)
+                const uint64_t m = __builtin_amdgcn_read_exec();
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                uint32_t b0 = 0;
+                if (rk == 0u) b0 = uint32_t(atomicAdd(mig_pool(kp), (unsigned long long)__builtin_popcountll(m)));
+                uint4* const rec = mig_rec(kp, __builtin_amdgcn_readfirstlane(b0) + rk);
+                uint32_t* const w = reinterpret_cast<uint32_t*>(rec);
+                const uint32_t v[21] = {__float_as_uint(ray.o.x), __float_as_uint(ray.o.y), __float_as_uint(ray.o.z),
+                                        __float_as_uint(ray.d.x), __float_as_uint(ray.d.y), __float_as_uint(ray.d.z),
+                                        __float_as_uint(thr.x), __float_as_uint(thr.y), __float_as_uint(thr.z),
+                                        __float_as_uint(col.x), __float_as_uint(col.y), __float_as_uint(col.z),
+                                        __float_as_uint(acc_rough), fs, bounce, smp.frame, smp.pixel, smp.offset,
+                                        uint32_t(ms.s), uint32_t(ms.s >> 32), uint32_t(ms.sp)};
+#pragma unroll
+                for (int k = 0; k < 21; ++k) mig_st(w + k, v[k]);
+                mig_drain();  // the record's words are out before its flag
+                mig_st(w + 24, slot + 1u);
+                alive = false;
+                work = false;
+            }
+#endif
 #if HG_RAY_SORT
             began = alive;
 #else
@@ -1321,6 +1507,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             if (out == gridDim.x - 1u) {
                 for (uint32_t h = 0; h < 8u; ++h)
                     __hip_atomic_store(kp.queue + 32u * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if HG_MIG_KERNEL
+                __hip_atomic_store(mig_state(kp), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(mig_pool(kp), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                 __hip_atomic_store(kp.queue + HG_QUEUE_DONE_WORD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }

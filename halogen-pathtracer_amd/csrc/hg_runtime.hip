@@ -1139,8 +1139,13 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     if (!rc && hipMemsetAsync(L.order_scratch.p, 0, L.order_scratch.bytes, L.stream) != hipSuccess)
                         rc = fail(c, HG_E_HIP, "hipMemsetAsync(order scratch) failed");
                 }
-                if (!rc && stream_k && L.queue.bytes < HG_QUEUE_BYTES) {
-                    rc = ensure_quiet(c, L.queue, HG_QUEUE_BYTES);
+#if HG_PATH_MIGRATE
+                const size_t qbytes = HG_QUEUE_BYTES_MIG(uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES);
+#else
+                const size_t qbytes = HG_QUEUE_BYTES;
+#endif
+                if (!rc && stream_k && L.queue.bytes < qbytes) {
+                    rc = ensure_quiet(c, L.queue, qbytes);
                     if (!rc && hipMemsetAsync(L.queue.p, 0, L.queue.bytes, L.stream) != hipSuccess)
                         rc = fail(c, HG_E_HIP, "hipMemsetAsync(queue) failed");
                 }
