@@ -238,6 +238,9 @@
 // The queue of a kQueue launch: 8 unit heads, 128 B apart (words 32 h), then the count of waves that have left (its own
 // 128-B line): the last wave out zeroes them for the next launch (the runtime zeroes the buffer once, at allocation)
 #define HG_QUEUE_DONE_WORD 256u
+#ifndef HG_QUEUE_DONE_RELAXED
+#define HG_QUEUE_DONE_RELAXED 0
+#endif
 #ifndef HG_PATH_MIGRATE
 #define HG_PATH_MIGRATE 0  // kQueue drain: waves left with few paths hand them to other waves at ray boundaries (§4.6)
 #endif

@@ -1502,8 +1502,14 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         // once its pulls found the queue dry, and it pulls no more after that: every head access of the launch
         // happens before the last wave's increment of the exit count (release / acquire).
         if (lane == 0u) {
+#if HG_QUEUE_DONE_RELAXED  // (A/B) the head atomics all returned before each wave's increment: no L2 write-back /
+                           // invalidate of the XCD per wave leaving
+            const uint32_t out = __hip_atomic_fetch_add(kp.queue + HG_QUEUE_DONE_WORD, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+#else
             const uint32_t out = __hip_atomic_fetch_add(kp.queue + HG_QUEUE_DONE_WORD, 1u, __ATOMIC_ACQ_REL,
                                                         __HIP_MEMORY_SCOPE_AGENT);
+#endif
             if (out == gridDim.x - 1u) {
                 for (uint32_t h = 0; h < 8u; ++h)
                     __hip_atomic_store(kp.queue + 32u * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
