@@ -54,9 +54,8 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
 # The traversal is bound by this unit (TD busy ~0.96), DESIGN.md sections 4.5, 10.
 VMEM_FLOOR_CYCLES = 20.0
 VMEM_PEAK_GINST = 256 * 2.4 / VMEM_FLOOR_CYCLES
-KERNEL_SYMBOL = {abi.HG_KERNEL_MEGA_POOL: "hg_trace_pool_kernel", abi.HG_KERNEL_MEGA_STREAM: "hg_trace_stream_kernel",
-                 abi.HG_KERNEL_MEGA_REGEN: "hg_trace_regen_kernel", abi.HG_KERNEL_MEGA: "hg_trace_kernel",
-                 abi.HG_KERNEL_WAVEFRONT: "hg_wf_trace"}
+KERNEL_SYMBOL = {abi.HG_KERNEL_MEGA_STREAM: "hg_trace_stream_kernel", abi.HG_KERNEL_MEGA_REGEN: "hg_trace_regen_kernel",
+                 abi.HG_KERNEL_MEGA: "hg_trace_kernel"}
 METRIC = "Mpaths/s (+ Mrays/s) at 1080p, 8-bounce dragon Cornell box, 1/2/4/8 GPU"
 
 
@@ -296,7 +295,7 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
         t = Transform((pos0[0] + 0.002 * k, pos0[1], pos0[2] - 0.001 * k), tuple(base.transform.rotation))
         return rp.Camera(t, base.fieldOfView, W, H)
 
-    def frame_loop(n: int):
+    def frame_loop(n: int, generation: int):
         before = ctx.counters()
         up = 0.0
         pending = 0
@@ -304,7 +303,7 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
         t0 = time.perf_counter()
         for k in range(n):
             tu = time.perf_counter()
-            ctx.upload_scene(packed)
+            ctx.upload_scene(packed, generation)
             up += time.perf_counter() - tu
             ctx.set_params(rp.make_params(s, camera_at(k + 1), 1, len(packed.spheres), len(packed.meshes),
                                           cube is not None))
@@ -323,8 +322,12 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
         return dt, up, after["scene_uploads_skipped"] - before["scene_uploads_skipped"], \
             after["scene_uploads"] - before["scene_uploads"]
 
-    frame_loop(4)  # warm-up
-    dt, up, skipped, rebuilt = frame_loop(frames)
+    # the drop-in passes' call: the geometry generation unchanged (their mesh registry did not change), so only the small
+    # arrays are compared (hg_upload_scene_gen); untagged, the 78 MB of triangles and BVH entries are compared as well
+    ctx.upload_scene(packed, 1)
+    frame_loop(4, 1)  # warm-up
+    dt, up, skipped, rebuilt = frame_loop(frames, 1)
+    dt0, up0, _, _ = frame_loop(frames, 0)
 
     def copy(p):
         arrays = {}
@@ -341,29 +344,34 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
     rebuild = []
     for k in range(4):
         t0 = time.perf_counter()
-        ctx.upload_scene(alt if k % 2 == 0 else packed)
+        ctx.upload_scene(alt if k % 2 == 0 else packed)  # (a new geometry: untagged)
         rebuild.append(time.perf_counter() - t0)
     # an object moved (the last mesh translated, then back): triangles and BVH as before, a partial re-upload
     moved = copy(packed)
     moved.meshes[len(moved.meshes) - 1].worldToLocal.m[12] += 0.05
     partial = []
+    ctx.upload_scene(packed, 2)
     for k in range(4):
         t0 = time.perf_counter()
-        ctx.upload_scene(moved if k % 2 == 0 else packed)
+        ctx.upload_scene(moved if k % 2 == 0 else packed, 2)  # (triangles and BVH vouched for: generation unchanged)
         partial.append(time.perf_counter() - t0)
     ctx.upload_scene(packed)
     c = ctx.counters()
     scene_bytes = sum(C.sizeof(getattr(packed, k)) for k in ("spheres", "meshes", "materials", "triangles", "blas"))
-    return {"workload": f"{frames} frames, camera moved before each: hg_upload_scene (same arrays) + hg_set_params + "
+    return {"workload": f"{frames} frames, camera moved before each: hg_upload_scene_gen (same arrays, same geometry "
+                        f"generation) + hg_set_params + "
                         f"hg_clear_accumulation + hg_render(1) + R11G11B10F display one frame behind (RP:262-299)",
             "value": W * H * frames / dt / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt * 1e3 / frames,
             "upload_ms_per_frame": up * 1e3 / frames, "upload_share": up / dt,
+            "untagged": {"value": W * H * frames / dt0 / 1e6, "ms_per_frame": dt0 * 1e3 / frames,
+                         "upload_ms_per_frame": up0 * 1e3 / frames, "upload_share": up0 / dt0,
+                         "note": "hg_upload_scene without a geometry generation: every array compared byte for byte"},
             "uploads_skipped": skipped, "uploads_rebuilt": rebuilt, "scene_bytes": scene_bytes,
             "changed_upload_ms": [x * 1e3 for x in rebuild],
             "changed_upload_ms_mean": sum(rebuild) * 1e3 / len(rebuild),
             "object_moved_upload_ms": [x * 1e3 for x in partial],
             "object_moved_upload_ms_mean": sum(partial) * 1e3 / len(partial),
-            "scene_uploads_partial": c["scene_uploads_partial"],
+            "scene_uploads_partial": c["scene_uploads_partial"], "scene_uploads_vouched": c["scene_uploads_vouched"],
             "scene_uploads_total": c["scene_uploads"], "host_threads_upload": 16}
 
 
@@ -539,11 +547,9 @@ def main():
     ap.add_argument("--readback-depth", type=int, default=2, help="--per-frame-only, --display pipelined: readbacks "
                     "in flight (HG_OPT_READBACK_DEPTH)")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", default="auto", choices=["auto", "wavefront", "mega", "regen", "stream", "pool"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "mega", "regen", "stream"])
     ap.add_argument("--frames-per-step", type=int, default=64,
                     help="progressive 1-spp frames per step per GPU-equivalent (64 = one C3 image)")
-    ap.add_argument("--timing", action="store_true", help="time every traversal launch (roofline of hg_wf_trace)")
-    ap.add_argument("--refill", type=int, default=0)
     ap.add_argument("--no-counters", action="store_true")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -561,6 +567,8 @@ def main():
     ap.add_argument("--wave-units", type=int, default=-1, help="HG_OPT_WAVE_UNITS (0 auto, k tiles per wave); -1: default")
     ap.add_argument("--lane-pick", type=int, default=-1, help="HG_OPT_LANE_PICK (0 in turn, 1 first idle); -1: default")
     ap.add_argument("--readback-stream", type=int, default=0, help="--per-frame-only: HG_OPT_READBACK_STREAM (1 side)")
+    ap.add_argument("--server", type=int, default=-1, help="HG_OPT_SERVER (1: the render server for calls of few frames, "
+                    "the default; 0: every call launches); -1: default")
     ap.add_argument("--bvh", default="reference", choices=["reference", "sah"],
                     help="BLAS builder of the timed scene: the reference's (the drop-in's parity path, the contract line) "
                          "or hg_build_blas_sah (NOT the reference's hierarchy; A/B and the fast_bvh leg)")
@@ -610,16 +618,12 @@ def main():
     params = rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None)
 
     ctx = abi.Context(device)
-    ctx.set_option(abi.HG_OPT_KERNEL, {"auto": abi.HG_KERNEL_AUTO, "wavefront": abi.HG_KERNEL_WAVEFRONT,
-                                       "mega": abi.HG_KERNEL_MEGA,
-                                       "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
-                                       "pool": abi.HG_KERNEL_MEGA_POOL}[args.kernel])
+    ctx.set_option(abi.HG_OPT_KERNEL, {"auto": abi.HG_KERNEL_AUTO, "mega": abi.HG_KERNEL_MEGA,
+                                       "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM}[args.kernel])
     # HIP events around every trace-kernel launch, on the trace stream it runs on (hg_counters.trace_ms): the roofline's
     # launch duration.  (kernel_ms spans a launch from its trace's start to its blend's end; consecutive launches
     # overlap on the two trace streams, so those spans overlap too.)
     ctx.set_option(abi.HG_OPT_TIMING, 1)
-    if args.refill:
-        ctx.set_option(abi.HG_OPT_REFILL, args.refill)
     if args.block:
         ctx.set_option(abi.HG_OPT_BLOCK, args.block)
     if args.frame_split >= 0:
@@ -630,6 +634,8 @@ def main():
         ctx.set_option(abi.HG_OPT_WAVE_UNITS, args.wave_units)
     if args.lane_pick >= 0:
         ctx.set_option(abi.HG_OPT_LANE_PICK, args.lane_pick)
+    if args.server >= 0:
+        ctx.set_option(abi.HG_OPT_SERVER, args.server)
     if args.descent_t >= -1:
         ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
@@ -711,6 +717,7 @@ def main():
         c = ctx.counters()
         print(json.dumps({"per_frame_only": True, "value": W * H * frames_per_step * args.steps / dt / 1e6,
                           "unit": "Mpaths/s", "launches": c["launches"], "ms_per_step": dt * 1e3 / args.steps,
+                          "server_launches": c["server_launches"], "server_frames": c["server_frames"],
                           "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1),
                           "host_ms_per_call": {k: v * 1e3 / n_calls for k, v in host.items()}}), flush=True)
         ctx.close()

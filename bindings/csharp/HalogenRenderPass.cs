@@ -15,15 +15,18 @@
 // frame over RCCL (hg_comm_init_all / hg_comm_gather); the image is identical to a one-GPU render.
 //
 // Display (RP:343-347): each frame's display readback is enqueued on the GPU (hg_readback_begin_format, or
-// hg_comm_readback_begin after the gather) and the image of HALOGEN_DISPLAY_LATENCY frames ago (default 1: one frame
-// behind) is shown, so the next frame traces while this one crosses PCIe.  The image comes in the format of the
-// reference's camera target, R11G11B10 float (URP-HighFidelity.asset:26-27, 4 B per pixel; HALOGEN_DISPLAY_FORMAT =
-// r11g11b10f | rgba16f | rgba32f), packed on the GPU; the fp32 accumulation target itself is never changed.
+// hg_comm_readback_begin after the gather) and the image of HALOGEN_DISPLAY_LATENCY frames ago is shown: 0, the
+// default, is the reference's (the frame just traced, RP:343-345); k > 0 opts into showing k frames behind while the
+// next frames trace.  After a ClearAccumulation the readbacks in flight are ended unseen and the next frame is shown at
+// once, so an image from before a camera move is never shown.  The image comes in the format of the reference's camera
+// target, R11G11B10 float (URP-HighFidelity.asset:26-27, 4 B per pixel; HALOGEN_DISPLAY_FORMAT = r11g11b10f | rgba16f |
+// rgba32f; any other value is an error), packed on the GPU; the fp32 accumulation target itself is never changed.
 //
 // No C# toolchain exists in the build image: this file is checked textually (public surface, the ABI calls it makes
 // exist in HalogenNative.cs and the header), not compiled.
 using System;
 using System.Collections.Generic;
+using System.Linq;
 using System.Runtime.InteropServices;
 using Unity.Mathematics;
 using UnityEngine;
@@ -103,6 +106,7 @@ public class HalogenRenderPass : ScriptableRenderPass
     readonly int displayFormat;      // HG_DISPLAY_* (HALOGEN_DISPLAY_FORMAT)
     readonly int displayLatency;     // frames the shown image lags the traced one (HALOGEN_DISPLAY_LATENCY)
     int displayPending;              // display readbacks enqueued and not yet shown
+    bool displayResync;              // the first frame after a clear is shown at once
     readonly ProfilingSampler sampler = new ProfilingSampler("Halogen (MI355X)");
 
     // scene lists, rebuilt by UpdateObjectBuffers
@@ -112,6 +116,11 @@ public class HalogenRenderPass : ScriptableRenderPass
     readonly List<HalogenTriangle> triangles = new List<HalogenTriangle>();
     readonly List<BVHEntry> blas = new List<BVHEntry>();
     readonly List<HalogenMaterial> seenMaterials = new List<HalogenMaterial>();
+    // the geometry generation of hg_upload_scene_gen: bumped whenever the mesh registry's members (instance, triangle
+    // count, BVH size, in order) differ from the last upload's; equal, it vouches for the 78 MB of triangles and BVH
+    // entries the reference re-uploads on every camera move (RP:262-268, 296-299), which the library then skips comparing
+    readonly List<long> geometrySignature = new List<long>();
+    ulong geometryGeneration;
 
     public HalogenRenderPass(ref HalogenSettings _settings)
     {
@@ -129,11 +138,14 @@ public class HalogenRenderPass : ScriptableRenderPass
         }
 
         string fmt = (Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_FORMAT") ?? "r11g11b10f").ToLowerInvariant();
-        displayFormat = fmt == "rgba32f" ? HalogenNative.HG_DISPLAY_RGBA32F
-                      : fmt == "rgba16f" ? HalogenNative.HG_DISPLAY_RGBA16F : HalogenNative.HG_DISPLAY_R11G11B10F;
-        int latency = 1;
-        int.TryParse(Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_LATENCY") ?? "1", out latency);
-        displayLatency = Math.Min(Math.Max(latency, 0), HalogenNative.HG_READBACK_MAX - 1);
+        if (fmt == "rgba32f") displayFormat = HalogenNative.HG_DISPLAY_RGBA32F;
+        else if (fmt == "rgba16f") displayFormat = HalogenNative.HG_DISPLAY_RGBA16F;
+        else if (fmt == "r11g11b10f") displayFormat = HalogenNative.HG_DISPLAY_R11G11B10F;
+        else throw new ArgumentException($"HALOGEN_DISPLAY_FORMAT '{fmt}': expected r11g11b10f, rgba16f or rgba32f");
+        string lat = Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_LATENCY") ?? "0";
+        if (!int.TryParse(lat, out int latency) || latency < 0 || latency >= HalogenNative.HG_READBACK_MAX)
+            throw new ArgumentException($"HALOGEN_DISPLAY_LATENCY '{lat}': expected 0..{HalogenNative.HG_READBACK_MAX - 1}");
+        displayLatency = latency;
         // the display ring lives on the context that displays (device 0; the gather's root)
         Check(HalogenNative.hg_set_option(contexts[0], HalogenNative.HG_OPT_READBACK_DEPTH, displayLatency + 1),
               "hg_set_option(HG_OPT_READBACK_DEPTH)");
@@ -185,6 +197,22 @@ public class HalogenRenderPass : ScriptableRenderPass
         FrameCount = 1;
         AccumulationBufferDirty = true;
         ObjectBuffersDirty = true;
+        DropDisplay();
+    }
+
+    // The display readbacks in flight show images from before a clear: end them unseen, and show the next frame at once
+    void DropDisplay()
+    {
+        for (; displayPending > 0; displayPending--)
+        {
+            IntPtr image;
+            UIntPtr nBytes;
+            int format;
+            int rc = comm != IntPtr.Zero ? HalogenNative.hg_comm_readback_end(comm, out image, out nBytes, out format)
+                                         : HalogenNative.hg_readback_end_data(contexts[0], out image, out nBytes, out format);
+            if (rc != HalogenNative.HG_OK) throw new Exception($"display readback failed ({rc})");
+        }
+        displayResync = displayLatency > 0;
     }
 
     // ---------------------------------------------------------------- one frame (RP:270-357)
@@ -271,7 +299,10 @@ public class HalogenRenderPass : ScriptableRenderPass
             Check(HalogenNative.hg_readback_begin_format(contexts[0], displayFormat), "hg_readback_begin_format");
         }
         displayPending++;
-        if (displayPending <= displayLatency) return;  // the pipeline fills: keep showing the previous image
+        if (displayResync)  // the first frame after a clear: its own image at once (the older ones were dropped)
+            displayResync = false;
+        else if (displayPending <= displayLatency)
+            return;  // the pipeline fills: keep showing the previous image
         IntPtr image;
         UIntPtr nBytes;
         int format;
@@ -312,6 +343,7 @@ public class HalogenRenderPass : ScriptableRenderPass
                 boundingCornerA = c - Vector3.one * r, boundingCornerB = c + Vector3.one * r,
             });
         }
+        var signature = new List<long>();
         foreach (RayTracingMesh m in RayTracingManager.GetMeshList().Values)
         {
             uint mat = MaterialSlot(m.material);
@@ -319,6 +351,15 @@ public class HalogenRenderPass : ScriptableRenderPass
             triangles.AddRange(m.GetPackedTriangles());
             meshes.Add(m.GetRefreshedMeshData(mat, triOffset, nodeOffset));
             blas.AddRange(m.GetBVH());
+            signature.Add(m.GetInstanceID());
+            signature.Add(triangles.Count - triOffset);
+            signature.Add(blas.Count - nodeOffset);
+        }
+        if (geometryGeneration == 0 || !signature.SequenceEqual(geometrySignature))
+        {
+            geometryGeneration++;
+            geometrySignature.Clear();
+            geometrySignature.AddRange(signature);
         }
         sceneSpheres = spheres.Count;
         sceneMeshes = meshes.Count;
@@ -331,8 +372,9 @@ public class HalogenRenderPass : ScriptableRenderPass
         BVHEntry[] nodes = blas.ToArray();
         foreach (IntPtr ctx in contexts)
         {
-            Check(HalogenNative.hg_upload_scene(ctx, sph, sph.Length, msh, msh.Length, mats, mats.Length, tris,
-                                                tris.Length, nodes, nodes.Length), "hg_upload_scene");
+            Check(HalogenNative.hg_upload_scene_gen(ctx, geometryGeneration, sph, sph.Length, msh, msh.Length, mats,
+                                                    mats.Length, tris, tris.Length, nodes, nodes.Length),
+                  "hg_upload_scene_gen");
             if (cfg.useCubemap && !cubemapUploaded) UploadCubemap(ctx);
         }
         cubemapUploaded = cfg.useCubemap;

@@ -23,15 +23,15 @@ struct hg_ctx {
 
     // scene
     bool has_scene = false;
-    DevBuf spheres, meshes, materials, nodes, leaves, tri_a, tri_b, tri_c, normals;
+    DevBuf spheres, meshes, materials, nodes, leaves, tris, normals;
     int32_t n_spheres = 0, n_meshes = 0, n_materials = 0, n_tris = 0, n_nodes = 0;
     uint32_t stack_depth = 2;
-    uint32_t hot_records = 0;  // HG_NODE_CACHE: device records [0, hot_records) are the BLAS tops (hot_prefix)
     // the caller's arrays of the last upload (spheres, meshes, materials, triangles, BVH entries), byte for byte: an
     // identical re-upload (the reference re-uploads on every camera move) is detected and skipped
     std::vector<uint8_t> scene_copy[5];
     std::vector<HgDevMesh> dev_meshes;  // the device mesh table of the last upload (partial re-uploads start from it)
-    uint64_t scene_uploads = 0, scene_uploads_skipped = 0, scene_uploads_partial = 0;
+    uint64_t scene_uploads = 0, scene_uploads_skipped = 0, scene_uploads_partial = 0, scene_uploads_vouched = 0;
+    uint64_t geometry_gen = 0;  // hg_upload_scene_gen: the caller's geometry generation of the last upload (0: none)
 
     // cubemap
     DevBuf cube;
@@ -46,11 +46,7 @@ struct hg_ctx {
     int32_t W = 0, H = 0, rank = 0, n_ranks = 1, tiles_x = 0, tiles_y = 0, n_local_tiles = 0;
     DevBuf acc;
 
-    // wavefront pipeline state (hg_wavefront.hip), sized for the local pixel slots
-    DevBuf wf_o, wf_d, wf_thr, wf_col, wf_sum, wf_st, wf_st2, wf_ms, wf_tuvo, wf_id, wf_q0, wf_q1;
-    DevBuf wf_counts, wf_heads;  // per bounce iteration: queue length, dequeue head
-    DevBuf wf_spill;             // traversal stack entries beyond HG_LDS_STACK, per trace thread
-    DevBuf pool;                 // path-pool kernel: per-wave path slots
+    DevBuf spill;  // traversal stack entries beyond the LDS part, per thread, of launches on the context stream
     // Trace pipeline (hg_render): the regenerating / streaming kernels trace each launch chunk on one of HG_TRACE_LANES
     // side streams, in turn, into that stream's own frame-colour buffer; the chunk's in-order blend into the accumulator
     // runs on `stream`.  So a chunk's tail overlaps the next chunk's trace, and everything else on `stream` (readback,
@@ -78,20 +74,41 @@ struct hg_ctx {
     TraceLane lanes[HG_TRACE_LANES];
     int next_lane = 0;     // chunks of at most HG_QUEUE_MAX_FRAMES frames: every lane in turn
     int next_lane_big = 0;  // longer chunks: lanes [0, HG_TRACE_LANES_BIG) in turn
-    uint32_t* poll_host = nullptr;  // pinned copies of queue lengths, polled to stop launching early
-    size_t poll_cap = 0;
-    std::vector<hipEvent_t> poll_events;
+
+    // The render server (hg_mega.hip kServer): launches of the reference's one frame per call
+    // (at most HG_QUEUE_MAX_FRAMES frames, accumulating, streaming kernel) post their frames to persistent trace waves
+    // that outlive the call, instead of launching; each frame's blend runs on `stream` behind a gate on its completion
+    // count.  Stopped (the waves drain what was posted and leave) by every entry point that changes what the waves
+    // read, by another kind of launch, and when its parameters or FrameCount chain do not continue.
+    struct Server {
+        hipStream_t stream = nullptr;  // CU-masked: a hardware queue of its own (never ahead of `stream`'s gates)
+        bool running = false;
+        DevBuf ctl;         // heads, mirror, ticket (HG_SV_CTL_BYTES), zeroed before each launch
+        DevBuf done;        // per ring slot a completion count on its own 128-B line, zeroed before each launch
+        DevBuf ring;        // colour ring: ring_n frames of n_local_tiles * 64 float4
+        DevBuf spill, tile_cost, tile_order, order_scratch;
+        bool tile_cost_valid = false;
+        unsigned long long* host = nullptr;  // pinned: [0] the post word (frames | stop << 32), [1] a gate's timeout
+        uint32_t ring_n = 0, posted = 0, cap = 0;
+        uint32_t uses[HG_SV_RING] = {};     // frames posted to each ring slot in this lifetime
+        hipEvent_t blended[HG_SV_RING] = {};  // after the blend of each ring slot's last frame
+        bool blend_valid[HG_SV_RING] = {};
+        hg_params params{};   // the parameters it was started with (frameCount: its first frame)
+        int32_t kernel_variant = 0, descent_t = 0;
+        HgKernelParams kp{};  // the launch's parameters (the blends read acc / ring / first_frame)
+        double last_post_s = 0.0;  // host clock of the last post
+    } sv;
+    int32_t server_on = 1;  // HG_OPT_SERVER
+    uint64_t server_launches = 0, server_frames = 0;
 
     // counters / timing
     DevBuf counters_dev;
-    DevBuf timeline;  // HG_WAVE_TIMELINE analysis builds: the queue waves' times of the last launches
-    uint64_t timeline_launches = 0;
     hg_counters counters{};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, free_events, pending_trace;
 
     // device / options
     int n_cu = 0;
-    int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0, refill = 32;
+    int32_t kernel = HG_KERNEL_AUTO, block = 128, counters_on = 1, timing = 0;
     int32_t frame_split = 0;  // 0: automatic (see hg_render)
     int32_t wave_units = 0;   // HG_OPT_WAVE_UNITS, 0: automatic (see hg_render)
     int32_t lane_pick = HG_LANE_PICK;  // HG_OPT_LANE_PICK: 1-frame chunks on the first idle trace stream (1) or in turn (0)

@@ -1,5 +1,5 @@
-// hg_device.h — device-side building blocks of the Halogen hot path shared by the kernels
-// (hg_mega.hip: one-thread-per-pixel megakernel; hg_wavefront.hip: regenerating wavefront pipeline).
+// hg_device.h — device-side building blocks of the Halogen hot path shared by the kernels of hg_mega.hip
+// (lockstep, regenerating and streaming megakernels, and the render server's persistent form of the streaming one).
 //
 // Every function restates a piece of the reference (file:line in its comment) in the reference's
 // operation order, compiled with -ffp-contract=off and the shared arithmetic spec include/hg_fmath.h, so the
@@ -32,12 +32,8 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
 }
 __device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
 __device__ __forceinline__ float rcp_exact(float x);
-// normalize = v * (1/sqrt(dot(v,v))) (hg_fmath.h hg_rnorm) with the correctly rounded reciprocal (same bits)
-#if HG_RCP_NORMALIZE
-__device__ __forceinline__ f3 normalize(f3 a) { return a * rcp_exact(__builtin_sqrtf(dot(a, a))); }
-#else
+// normalize = v * (1/sqrt(dot(v,v))) (hg_fmath.h hg_rnorm)
 __device__ __forceinline__ f3 normalize(f3 a) { return a * hg_rnorm(dot(a, a)); }
-#endif
 __device__ __forceinline__ f3 lerp(f3 a, f3 b, float s) { return a + (b - a) * s; }
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 
@@ -104,19 +100,6 @@ struct Sampler {
 constexpr uint32_t ID_FOCAL = 0, ID_JITTER = 1, ID_ROUGH = 2, ID_PROPERTY = 3, ID_RR = 4, BOUNCE_INC = 5;
 #define HLSL_PI (180.0f * HG_DEG2RAD)
 
-// XCD-aware block order: the dispatcher deals workgroups round-robin to the 8 XCDs (b % 8), each with its own
-// L2.  Remapping b -> a contiguous range per XCD gives every XCD its own band of tiles, so the BVH nodes its
-// waves touch overlap more in its L2.  A bijection on [0, n) whatever the real placement (speed only).
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
-#if HG_XCD_REMAP
-    const uint32_t xcd = b & 7u, k = b >> 3, per = n >> 3, rem = n & 7u;
-    return xcd < rem ? xcd * (per + 1u) + k : rem * (per + 1u) + (xcd - rem) * per + k;
-#else
-    (void)n;
-    return b;
-#endif
-}
-
 // ---------------------------------------------------------------------------------------------------
 // Per-lane path state
 // ---------------------------------------------------------------------------------------------------
@@ -132,14 +115,6 @@ __device__ __forceinline__ uint64_t wave_clock() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
     return t;
-}
-// HG_PHASE_DETAIL analysis builds: add the wave clock elapsed since `since` to counter slot `slot` (from the first
-// active lane, so it works inside divergent code) and return the new clock.
-__device__ __forceinline__ uint64_t phase_mark(const HgKernelParams& kp, int slot, uint64_t since) {
-    const uint64_t t = wave_clock();
-    if (int(threadIdx.x & 63u) == __ffsll((unsigned long long)__ballot(1)) - 1)
-        atomicAdd(kp.counters + slot, (unsigned long long)(t - since));
-    return wave_clock();
 }
 // 64-lane ballot of a bool straight from the compare mask (the HIP __ballot(int) materialises the predicate in a
 // VGPR and compares it again)
@@ -184,18 +159,6 @@ struct Mat {
     float4 albedo, spec_metal, emis_rough, absorb_ior, prio_id_r2;
 };
 __device__ __forceinline__ Mat load_mat(const HgKernelParams& kp, uint32_t m) {
-#if HG_MAT_SCALAR
-    // every active lane shading the same material (one glass, one wall): five scalar loads through the constant
-    // cache instead of five vector-memory instructions on the texture-data unit that binds the kernel
-    const uint32_t m0 = uint32_t(__builtin_amdgcn_readfirstlane(int(m)));
-    if (__builtin_amdgcn_ballot_w64(m != m0) == 0ull) {
-        typedef const __attribute__((address_space(4))) float* cfp;
-        const cfp q = (cfp)(uintptr_t)(kp.materials + 5u * m0);
-        return Mat{make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]),
-                   make_float4(q[8], q[9], q[10], q[11]), make_float4(q[12], q[13], q[14], q[15]),
-                   make_float4(q[16], q[17], q[18], q[19])};
-    }
-#endif
     const float4* p = kp.materials + 5 * m;
     return Mat{p[0], p[1], p[2], p[3], p[4]};
 }
@@ -232,56 +195,38 @@ __device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
-// Frame colour of launch frame f (0 .. n_frames-1) for accumulator slot `slot` (hg_blend_frames reads the same layout)
-__device__ __forceinline__ size_t fc_slot_frame(size_t slot, uint32_t f, size_t n_slots, uint32_t n_frames) {
-#if HG_FC_SLOT_MAJOR
-    (void)n_slots;
+// Frame colour of launch frame f (0 .. n_frames-1) for accumulator slot `slot`: [slot][frame], one pixel's frames
+// contiguous (hg_blend_frames* read the same layout)
+__device__ __forceinline__ size_t fc_slot_frame(size_t slot, uint32_t f, uint32_t n_frames) {
     return slot * size_t(n_frames) + f;
-#else
-    (void)n_frames;
-    return size_t(f) * n_slots + slot;
-#endif
 }
-// Frame colours are written once by the trace and read once by the blend: with HG_FC_NT both go through the
-// non-temporal hint, so the 2.1 GB a 64-frame C3 launch writes is not kept in L2 ahead of the BVH lines
+// Frame colours are written once by the trace and read once by the blend: both go through the non-temporal hint, so
+// the 2.1 GB a 64-frame C3 launch writes is not kept in L2 ahead of the BVH lines (+0.2..0.6 %, sweep_r03_n)
 __device__ __forceinline__ void fc_store(float4* p, float4 v) {
-#if HG_FC_NT
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
     __builtin_nontemporal_store(v.z, &p->z);
     __builtin_nontemporal_store(v.w, &p->w);
-#else
-    *p = v;
-#endif
 }
 __device__ __forceinline__ float4 fc_load(const float4* p) {
-#if HG_FC_NT
     return make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
                        __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
-#else
-    return *p;
-#endif
 }
 __device__ __forceinline__ size_t fc_index(const HgKernelParams& kp, uint32_t f, size_t slot) {
-    return fc_slot_frame(slot, f, size_t(uint32_t(kp.n_local_tiles)) * 64u, uint32_t(kp.n_frames));
+    return fc_slot_frame(slot, f, uint32_t(kp.n_frames));
 }
 
-// Triangle ti's Moller-Trumbore operands from the three SoA streams: a = (v0, e1.x), b = (e1.yz, e2.xy), cz = e2.z.
-// (One 48-B record per triangle instead was measured: C3 -0.3 %, C2 -5.7 %, C5 -2.4 %, tools/sweeps/NOTES_r02.md;
-// the non-temporal hint on these loads: C3 -9.7 %, C3F -10 %, tools/sweeps/sweep_r03_o.jsonl.)
+// Triangle ti's Moller-Trumbore operands from its packed 36-B record (v0, e1, e2): a = (v0, e1.x), b = (e1.yz, e2.xy),
+// cz = e2.z, as two 4-B-aligned 16-B loads and one 4-B load.  (The three SoA streams of rounds 1-2 put a leaf's
+// triangles on 3-5 lines instead of 2-3: L1 misses -20 % with this record; 48-B padded records lost 0.3-5.7 %; the
+// non-temporal hint on these loads lost 10 %, a leaf's triangles are re-read by the next rounds and waves.)
 __device__ __forceinline__ void tri_load(const HgKernelParams& kp, uint32_t ti, float4& a, float4& b, float& cz) {
-#if HG_TRI_AOS
     typedef float hg_v4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned 16-B loads
-    const char* p = reinterpret_cast<const char*>(kp.tri_a) + ti * 36u;
+    const char* p = reinterpret_cast<const char*>(kp.tris) + ti * 36u;
     const hg_v4u va = *reinterpret_cast<const hg_v4u*>(p), vb = *reinterpret_cast<const hg_v4u*>(p + 16);
     a = make_float4(va.x, va.y, va.z, va.w);
     b = make_float4(vb.x, vb.y, vb.z, vb.w);
     cz = *reinterpret_cast<const float*>(p + 32);
-#else
-    a = ld_off(kp.tri_a, ti << 4);
-    b = ld_off(kp.tri_b, ti << 4);
-    cz = ld_off(kp.tri_c, ti << 2);
-#endif
 }
 
 // Load of scene data the kernel never writes (mesh records, spheres) through the constant address space: a
@@ -312,56 +257,22 @@ __device__ __forceinline__ float ray_aabb(f3 A, f3 B, f3 o, f3 inv) {  // :244-2
     return tMax > fmaxf(0.0f, tMin) ? tMin : HG_INF;
 }
 
-// A child-pair record (hg_runtime.hip, BLAS pass 2): both children's boxes and refs in 64 B, 56 of them used.
-// HG_PAIR_SOA lays the boxes out coordinate by coordinate with A and B side by side, so that the two box tests of a
-// descent step run on packed FP32 pairs (v_pk_add_f32 / v_pk_mul_f32: two IEEE operations per instruction, the same
-// results as the scalar ones):
-//   q0 = (A.lo.x, B.lo.x, A.lo.y, B.lo.y), q1 = (A.lo.z, B.lo.z, A.hi.x, B.hi.x), q2 = (A.hi.y, B.hi.y, A.hi.z, B.hi.z),
-//   q3 = (refA, refB, -, -);
-// otherwise q0 = (A.lo, refA), q1 = (A.hi, refB), q2 = (B.lo, -), q3 = (B.hi, -).
+// A child-pair record (hg_runtime.hip, BLAS pass 2): both children's boxes and refs in 64 B, 56 of them used:
+// q0 = (A.lo, refA), q1 = (A.hi, refB), q2 = (B.lo, -), q3 = (B.hi, -).  (The coordinate-by-coordinate form for packed
+// FP32 box tests cost 8-16 B of scratch and lost 1-2.4 %)
 struct NodePair {
     float4 q0, q1, q2, q3;
 };
 __device__ __forceinline__ NodePair node_pair(const HgKernelParams& kp, uint32_t node) {
     const uint32_t ro = node << 6;
-#if HG_PAIR_SOA
-    const uint2 refs = ld_off(reinterpret_cast<const uint2*>(kp.nodes), ro + 48);
-    return NodePair{ld_off(kp.nodes, ro), ld_off(kp.nodes, ro + 16), ld_off(kp.nodes, ro + 32),
-                    make_float4(__uint_as_float(refs.x), __uint_as_float(refs.y), 0.0f, 0.0f)};
-#else
     return NodePair{ld_off(kp.nodes, ro), ld_off(kp.nodes, ro + 16), ld_off(kp.nodes, ro + 32), ld_off(kp.nodes, ro + 48)};
-#endif
 }
-__device__ __forceinline__ NodePair node_pair_at(const float4* p) { return NodePair{p[0], p[1], p[2], p[3]}; }
-__device__ __forceinline__ uint32_t pair_ref_a(const NodePair& r) {
-    return __float_as_uint(HG_PAIR_SOA ? r.q3.x : r.q0.w);
-}
-__device__ __forceinline__ uint32_t pair_ref_b(const NodePair& r) {
-    return __float_as_uint(HG_PAIR_SOA ? r.q3.y : r.q1.w);
-}
+__device__ __forceinline__ uint32_t pair_ref_a(const NodePair& r) { return __float_as_uint(r.q0.w); }
+__device__ __forceinline__ uint32_t pair_ref_b(const NodePair& r) { return __float_as_uint(r.q1.w); }
 // ray_aabb (:244-259) of both children: dA, dB
 __device__ __forceinline__ void pair_dist(const NodePair& r, f3 o, f3 inv, float& dA, float& dB) {
-#if HG_PAIR_SOA
-    typedef float v2f __attribute__((ext_vector_type(2)));
-    const v2f lx = (v2f{r.q0.x, r.q0.y} - o.x) * inv.x, ly = (v2f{r.q0.z, r.q0.w} - o.y) * inv.y;
-    const v2f lz = (v2f{r.q1.x, r.q1.y} - o.z) * inv.z, hx = (v2f{r.q1.z, r.q1.w} - o.x) * inv.x;
-    const v2f hy = (v2f{r.q2.x, r.q2.y} - o.y) * inv.y, hz = (v2f{r.q2.z, r.q2.w} - o.z) * inv.z;
-    float aMin = fminf(lx.x, hx.x), aMax = fmaxf(lx.x, hx.x);
-    aMin = fmaxf(aMin, fminf(ly.x, hy.x));
-    aMax = fminf(aMax, fmaxf(ly.x, hy.x));
-    aMin = fmaxf(aMin, fminf(lz.x, hz.x));
-    aMax = fminf(aMax, fmaxf(lz.x, hz.x));
-    float bMin = fminf(lx.y, hx.y), bMax = fmaxf(lx.y, hx.y);
-    bMin = fmaxf(bMin, fminf(ly.y, hy.y));
-    bMax = fminf(bMax, fmaxf(ly.y, hy.y));
-    bMin = fmaxf(bMin, fminf(lz.y, hz.y));
-    bMax = fminf(bMax, fmaxf(lz.y, hz.y));
-    dA = aMax > fmaxf(0.0f, aMin) ? aMin : HG_INF;
-    dB = bMax > fmaxf(0.0f, bMin) ? bMin : HG_INF;
-#else
     dA = ray_aabb(xyz(r.q0), xyz(r.q1), o, inv);
     dB = ray_aabb(xyz(r.q2), xyz(r.q3), o, inv);
-#endif
 }
 
 // Returns the closest accepted sphere as index | (orientation < 0) << 31 (HG_NONE if none), its distance in t;
@@ -738,9 +649,13 @@ __device__ __forceinline__ bool leaf_dist(const HgKernelParams& kp, const LeafRa
 }
 
 // get_ray_scene_intersection_mesh, :378-472.
-// The mesh loop is wave-uniform (mesh records come through the scalar cache); inside a mesh the traversal keeps
-// the current node in a register (the reference's push-near-then-pop-near is a no-op on order) and runs
-// while-while: all lanes descend inner nodes together until each holds a leaf, then test one leaf each.
+// Per-lane mesh cursor: each lane walks its own live meshes in buffer order (the reference's order, so ties resolve
+// identically) and moves to its next mesh as soon as it finishes one, so a wave waits for the lane with the most total
+// work instead of the slowest lane of every mesh in turn.  Inside a mesh the traversal keeps the current node in a
+// register (the reference's push-near-then-pop-near is a no-op on order) and runs a relaxed while-while: the lanes
+// descend inner nodes together while more than kp.descent_t of them are still descending (0: until every lane is at a
+// leaf), and in any case until at least one lane can make other progress; then each tests its leaf.  Each lane's own
+// sequence of node / leaf steps is the reference's.
 template <bool kMeshLds = false, class Stk>
 __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, Counters& c, const Stk& stk) {
     const float eps = 0.0001f;
@@ -752,10 +667,6 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     const uint64_t live = mesh_live_mask(kp, ray.o, winv, best_t, culled);
     c.aabb += 2 * culled;
-#if HG_LANE_MESHES
-    // Per-lane mesh cursor: each lane walks its own live meshes in buffer order (the reference's order, so ties
-    // resolve identically) and moves to its next mesh as soon as it finishes one, so a wave waits for the lane
-    // with the most total work instead of the slowest lane of every mesh in turn.
     const uint32_t nm = uint32_t(kp.n_meshes);
     uint32_t mi = next_live_mesh(live, 0u, nm);
     bool active = mi < nm;
@@ -763,13 +674,6 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
     uint32_t node = HG_NONE, sp = 0;
     if (active) mesh_local_ray<kMeshLds>(kp, ray, mi, lo, ld, inv, node);
     while (__any(active)) {
-#if HG_TRAV_IFIF
-        if (active && !(node & HG_LEAF_BIT)) {  // if-if: one node step per round, leaves tested in the same round
-#else
-        // while-while, relaxed: descend while more than kp.descent_t lanes are still descending (0: until every
-        // lane is at a leaf), and in any case until at least one lane can make other progress (a leaf to test or
-        // its mesh finished); the few stragglers pause while the others test their leaves.  Each lane's own
-        // sequence of node / leaf steps is unchanged.
         const uint64_t act_mask = wave_ballot(active);
         const uint32_t dt = kp.descent_t;
         for (uint64_t dm = act_mask & wave_ballot(int32_t(node) >= 0);
@@ -777,7 +681,6 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
              dm = act_mask & wave_ballot(int32_t(node) >= 0)) {
             c.node_rounds += wave_once();
             if (active && int32_t(node) >= 0) {
-#endif
                 const NodePair np = node_pair(kp, node);
                 float dA, dB;
                 pair_dist(np, lo, inv, dA, dB);
@@ -787,12 +690,6 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 const bool bFirst = dB < dA;
                 const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
                 const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
-                // near (far pushed if it is also entered), else far, else pop — decided branch-free
-#if HG_BRANCHLESS_DESCENT
-                if (nearOk && farOk) stk.push(sp, farRef);
-                node = nearOk ? nearRef : farRef;
-                if (!nearOk && !farOk) node = sp > 0 ? stk.pop(sp) : HG_NONE;
-#else
                 if (nearOk) {
                     if (farOk) stk.push(sp, farRef);
                     node = nearRef;
@@ -801,33 +698,16 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
                 } else {
                     node = sp > 0 ? stk.pop(sp) : HG_NONE;
                 }
-#endif
-#if HG_TRAV_IFIF
-        } else
-#else
             }
         }
-#endif
         if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order (:404-420)
             const uint2 leaf = leaf_range(kp, node);
             const uint32_t end = leaf.x + leaf.y;
-#if HG_TRI_PREFETCH
-            float4 na, nb;
-            float nc;
-            tri_load(kp, leaf.x, na, nb, nc);
-#endif
             for (uint32_t ti = leaf.x; ti < end; ++ti) {
                 c.tri_rounds += wave_once();
-#if HG_TRI_PREFETCH  // the next triangle's loads go out before this one is tested
-                const float4 a = na, b = nb;
-                const float cz = nc;
-                const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
-                tri_load(kp, tn, na, nb, nc);
-#else
                 float4 a, b;
                 float cz;
                 tri_load(kp, ti, a, b, cz);
-#endif
                 c.tri++;
                 float t, U, V;
                 bool front;
@@ -847,83 +727,6 @@ __device__ bool isect_meshes(const HgKernelParams& kp, const Ray& ray, Hit& h, C
             else active = false;
         }
     }
-#else
-    for (int mi = 0; mi < kp.n_meshes; ++mi) {
-        bool active = mi >= 64 || ((live >> mi) & 1ull);
-        if (!__any(active)) continue;  // the whole wave skips this mesh
-        if (!active) continue;
-        const float4* md4 = reinterpret_cast<const float4*>(kp.meshes + mi);
-        const float4 c0 = md4[0], c1 = md4[1], c2 = md4[2], c3 = md4[3];  // worldToLocal columns
-        const uint32_t root = __float_as_uint(md4[4].x);
-        // world -> local, direction NOT normalized (:390-392)
-        const f3 lo = mk(((c0.x * ray.o.x + c1.x * ray.o.y) + c2.x * ray.o.z) + c3.x * 1.0f,
-                         ((c0.y * ray.o.x + c1.y * ray.o.y) + c2.y * ray.o.z) + c3.y * 1.0f,
-                         ((c0.z * ray.o.x + c1.z * ray.o.y) + c2.z * ray.o.z) + c3.z * 1.0f);
-        const f3 ld = mk(((c0.x * ray.d.x + c1.x * ray.d.y) + c2.x * ray.d.z) + c3.x * 0.0f,
-                         ((c0.y * ray.d.x + c1.y * ray.d.y) + c2.y * ray.d.z) + c3.y * 0.0f,
-                         ((c0.z * ray.d.x + c1.z * ray.d.y) + c2.z * ray.d.z) + c3.z * 0.0f);
-        const f3 inv = mk(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
-        uint32_t node = root, sp = 0;  // root pushed untested (:401), held in a register
-        while (__any(active)) {
-            while (__any(active && !(node & HG_LEAF_BIT))) {
-                if (active && !(node & HG_LEAF_BIT)) {
-                    const NodePair np = node_pair(kp, node);
-                    float dA, dB;
-                    pair_dist(np, lo, inv, dA, dB);
-                    c.aabb += 2;
-                    const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
-                    // reference (:430-444): push far, push near (each only if tEntry < closest), pop near
-                    const bool bFirst = dB < dA;
-                    const uint32_t nearRef = bFirst ? refB : refA, farRef = bFirst ? refA : refB;
-                    const bool nearOk = (bFirst ? dB : dA) < best_t, farOk = (bFirst ? dA : dB) < best_t;
-                    if (nearOk) {
-                        if (farOk) stk.push(sp, farRef);
-                        node = nearRef;
-                    } else if (farOk) {
-                        node = farRef;
-                    } else {
-                        node = sp > 0 ? stk.pop(sp) : HG_NONE;
-                    }
-                }
-            }
-            if (active && node != HG_NONE && (node & HG_LEAF_BIT)) {  // a leaf: its triangles in order
-                const uint2 leaf = leaf_range(kp, node);
-                uint32_t ti = leaf.x;
-                const uint32_t end = leaf.x + leaf.y;
-#if HG_TRI_PREFETCH
-                float4 ta, tb;
-                float tc;
-                tri_load(kp, ti, ta, tb, tc);
-#endif
-                for (; ti < end; ++ti) {
-#if HG_TRI_PREFETCH
-                    const float4 a = ta, b = tb;
-                    const float cz = tc;
-                    if (ti + 1 < end) {
-                        tri_load(kp, ti + 1, ta, tb, tc);
-                    }
-#else
-                    float4 a, b;
-                    float cz;
-                    tri_load(kp, ti, a, b, cz);
-#endif
-                    c.tri++;
-                    float t, U, V;
-                    bool front;
-                    if (tri_accept(lo, ld, a, b, cz, best_t, t, U, V, front)) {
-                        best_t = t;
-                        best_u = U;
-                        best_v = V;
-                        best_tri = ti | (front ? 0u : 0x80000000u);
-                        best_mesh = uint32_t(mi);
-                    }
-                }
-                node = sp > 0 ? stk.pop(sp) : HG_NONE;
-            }
-            if (node == HG_NONE) active = false;
-        }
-    }
-#endif
     // :452-471
     if (best_t < (h.t - eps) && best_t < kp.far_) {
         resolve_mesh<kMeshLds>(kp, ray, best_t, best_u, best_v, best_tri, best_mesh, h);
@@ -951,135 +754,6 @@ __device__ __forceinline__ Hit intersect(const HgKernelParams& kp, const Ray& ra
 // per-lane mesh cursor / while-while traversal as intersect(), with its state in a struct so a lane can stop
 // between steps (other lanes shade) and resume.  Same visit order, same counters, same result.
 // ---------------------------------------------------------------------------------------------------
-#if HG_NODE_PREFETCH
-// Prefetch the 128-B line holding the children's records (DFS pair layout: siblings share a line) while the
-// current record's boxes are tested: a 4-B load straight into a per-wave LDS sink (no VGPR is written), whose only
-// purpose is to pull the line into the caches before the next round asks for it.
-__shared__ uint32_t hg_prefetch_sink[64];
-__device__ __forceinline__ void node_prefetch(const HgKernelParams& kp, uint32_t refA, uint32_t refB) {
-    const uint32_t pf = !(refA & HG_LEAF_BIT) ? refA : refB;
-    if (!(pf & HG_LEAF_BIT))
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(uintptr_t)(reinterpret_cast<const char*>(kp.nodes) +
-                                                                       (size_t(pf) << 6)),
-            (__attribute__((address_space(3))) void*)hg_prefetch_sink, 4, 0, 0);
-}
-#endif
-
-#if HG_QUAD_FETCH
-// Quad-cooperative node fetch (DESIGN.md §10 lever 4).  A descent step loads one 64-B record per lane with four 16-B
-// loads, each touching up to 64 records per wave instruction, and the texture data path prices an instruction by the
-// lines it touches.  Here the four lanes of each quad load their four records one after another (round j: lane q loads
-// quarter q of quad-lane j's record, so an instruction touches at most 16 records, each as one contiguous 64 B), and a
-// 4x4 transpose inside the quad (two DPP butterfly stages) hands every lane its own record: the same bytes, the same
-// result.  Every lane of the wave must take part (trav_step runs with the whole wave active).
-template <int kCtrl>
-__device__ __forceinline__ uint32_t qperm(uint32_t v) {
-    return uint32_t(__builtin_amdgcn_mov_dpp(int(v), kCtrl, 0xF, 0xF, true));
-}
-template <int kCtrl>
-__device__ __forceinline__ float qpermf(float v) { return __uint_as_float(qperm<kCtrl>(__float_as_uint(v))); }
-// one butterfly stage over columns (a, b) = (j, j ^ s): a' = hi ? partner's b : a, b' = hi ? b : partner's a
-template <int kCtrl>
-__device__ __forceinline__ void quad_stage(float4& a, float4& b, bool hi) {
-    const float4 pa = make_float4(qpermf<kCtrl>(a.x), qpermf<kCtrl>(a.y), qpermf<kCtrl>(a.z), qpermf<kCtrl>(a.w));
-    const float4 pb = make_float4(qpermf<kCtrl>(b.x), qpermf<kCtrl>(b.y), qpermf<kCtrl>(b.z), qpermf<kCtrl>(b.w));
-    a = make_float4(hi ? pb.x : a.x, hi ? pb.y : a.y, hi ? pb.z : a.z, hi ? pb.w : a.w);
-    b = make_float4(hi ? b.x : pa.x, hi ? b.y : pa.y, hi ? b.z : pa.z, hi ? b.w : pa.w);
-}
-// The records of the lanes with `want` (others: unspecified); false = the caller loads per lane (adaptive mode chose
-// the per-lane path for this step)
-__device__ __forceinline__ bool quad_node_fetch(const HgKernelParams& kp, bool want, uint32_t node, float4& c0,
-                                                float4& c1, float4& c2, float4& c3) {
-    const uint32_t q = __lane_id() & 3u;
-    const uint32_t key = want ? node : HG_NONE;
-    const uint32_t k0 = qperm<0x00>(key), k1 = qperm<0x55>(key), k2 = qperm<0xAA>(key), k3 = qperm<0xFF>(key);
-#if HG_QUAD_FETCH == 2
-    // quads that need 2+ distinct records (where one full-record load per round beats four 64-record loads)
-    const bool spread = q == 0u && ((k1 != k0 && k1 != HG_NONE && k0 != HG_NONE) ||
-                                    (k2 != k0 && k2 != k1 && k2 != HG_NONE) ||
-                                    (k3 != k0 && k3 != k1 && k3 != k2 && k3 != HG_NONE));
-    if (wave_count(spread) < uint32_t(HG_QUAD_MIN)) return false;
-#endif
-    const uint32_t qo = q << 4;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
-    if (k0 != HG_NONE) r0 = ld_off(kp.nodes, (k0 << 6) + qo);
-    if (k1 != HG_NONE) r1 = ld_off(kp.nodes, (k1 << 6) + qo);
-    if (k2 != HG_NONE) r2 = ld_off(kp.nodes, (k2 << 6) + qo);
-    if (k3 != HG_NONE) r3 = ld_off(kp.nodes, (k3 << 6) + qo);
-    // r_j holds quarter q of quad-lane j's record; transpose so that lane q holds quarters 0..3 of its own
-    const bool h1 = (q & 1u) != 0u, h2 = (q & 2u) != 0u;
-    quad_stage<0xB1>(r0, r1, h1);  // quad_perm 1,0,3,2
-    quad_stage<0xB1>(r2, r3, h1);
-    quad_stage<0x4E>(r0, r2, h2);  // quad_perm 2,3,0,1
-    quad_stage<0x4E>(r1, r3, h2);
-    c0 = r0;
-    c1 = r1;
-    c2 = r2;
-    c3 = r3;
-    return true;
-}
-#endif
-
-#if HG_NODE_DEDUP
-// Wave-level deduplicated node fetch (DESIGN.md §10 lever 10).  A descent round's loading lanes need few distinct
-// records (C3: 5-16 in 48 % of rounds, 17-32 in 47 %, more in 0.07 %; tools/coherence_stats.py), yet each lane
-// loading its own 64-B record costs the texture-data unit four wave instructions whatever the sharing.  Here the
-// distinct records are enumerated (one readlane + ballot per record), packed densely into lanes (4 lanes x 16 B per
-// record when at most 16, else 2 lanes x 2 x 16 B), fetched with one or two wave instructions, and every lane takes
-// its record's 16 words from their lanes with ds_bpermute.  The same bytes: the same results.  Returns false (the
-// caller loads per lane) when more than 32 records are needed.  The whole wave must be active.
-__device__ __forceinline__ uint32_t bperm_u(uint32_t src_lane, uint32_t v) {
-    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src_lane << 2), int(v)));
-}
-__device__ __forceinline__ float4 bperm_f4(uint32_t src_lane, const float4& v) {
-    const int a = int(src_lane << 2);
-    return make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.x))),
-                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.y))),
-                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.z))),
-                       __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v.w))));
-}
-__device__ __forceinline__ bool wave_node_fetch(const HgKernelParams& kp, bool want, uint32_t node, NodePair& np) {
-    const uint32_t lane = __lane_id();
-    uint64_t m = wave_ballot(want);
-    uint32_t slot = 0u, list = 0u, k = 0u;
-    while (m != 0ull && k < 32u) {  // wave-uniform: one distinct record per iteration
-        const uint32_t first = uint32_t(__builtin_amdgcn_readlane(int(node), int(__builtin_ctzll(m))));
-        const bool same = want && node == first;
-        m &= ~wave_ballot(same);
-        slot = same ? k : slot;
-        list = lane == k ? first : list;
-        ++k;
-    }
-    if (m != 0ull) return false;
-    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (k <= 16u) {  // record j in lanes 4j .. 4j+3, 16 B each: one load instruction
-        const uint32_t rec = bperm_u(lane >> 2, list);
-        float4 a = z;
-        if ((lane >> 2) < k) a = ld_off(kp.nodes, (rec << 6) + ((lane & 3u) << 4));
-        const uint32_t s = slot << 2;
-        np.q0 = bperm_f4(s, a);
-        np.q1 = bperm_f4(s + 1u, a);
-        np.q2 = bperm_f4(s + 2u, a);
-        np.q3 = bperm_f4(s + 3u, a);
-    } else {  // record j in lanes 2j, 2j+1: bytes 0-15 / 16-31 (first load), 32-47 / 48-63 (second)
-        const uint32_t rec = bperm_u(lane >> 1, list);
-        float4 a = z, b = z;
-        if ((lane >> 1) < k) {
-            const uint32_t off = (rec << 6) + ((lane & 1u) << 4);
-            a = ld_off(kp.nodes, off);
-            b = ld_off(kp.nodes, off + 32u);
-        }
-        const uint32_t s = slot << 1;
-        np.q0 = bperm_f4(s, a);
-        np.q1 = bperm_f4(s + 1u, a);
-        np.q2 = bperm_f4(s, b);
-        np.q3 = bperm_f4(s + 1u, b);
-    }
-    return true;
-}
-#endif
-
 struct Trav {
     f3 lo, ld;             // ray in the current mesh's local space (1/ld is recomputed per round, trav_step)
     float best_t, best_u, best_v, sph_t;
@@ -1091,14 +765,8 @@ struct Trav {
 template <bool kMeshLds = false>
 __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& ray, Trav& t, Counters& c) {
     c.rays++;
-#if HG_PHASE_DETAIL == 2
-    uint64_t tp = wave_clock();
-#endif
     t.sph_t = HG_INF;
     t.sph = isect_spheres(kp, ray, t.sph_t);
-#if HG_PHASE_DETAIL == 2
-    if (kp.counters) tp = phase_mark(kp, 11, tp);
-#endif
     t.best_t = t.sph_t;  // closestIntersection.rayT starts at the sphere hit (:381)
     t.best_u = 0.0f;
     t.best_v = 0.0f;
@@ -1107,9 +775,6 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     uint32_t culled = 0;
     const f3 winv = mk(rcp_exact(ray.d.x), rcp_exact(ray.d.y), rcp_exact(ray.d.z));
     t.live = mesh_live_mask(kp, ray.o, winv, t.best_t, culled);
-#if HG_PHASE_DETAIL == 2
-    if (kp.counters) tp = phase_mark(kp, 12, tp);
-#endif
     c.aabb += 2 * culled;
     t.sp = 0;
     t.node = HG_NONE;
@@ -1117,12 +782,6 @@ __device__ __forceinline__ void trav_begin(const HgKernelParams& kp, const Ray& 
     t.mi = next_live_mesh(t.live, 0u, nm);
     f3 inv;
     if (t.mi < nm) mesh_local_ray<kMeshLds>(kp, ray, t.mi, t.lo, t.ld, inv, t.node);
-#if HG_PHASE_DETAIL == 2
-    if (kp.counters) {
-        asm volatile("" : : "v"(t.node), "v"(t.lo.x), "v"(t.ld.x));  // keep the loads' wait inside this phase
-        tp = phase_mark(kp, 13, tp);
-    }
-#endif
 }
 
 // One while-while round for the lanes with `act`: descend until each is at a leaf (or out of nodes), test that
@@ -1133,9 +792,6 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     // 1/ld (the same rcp_exact values mesh_local_ray computes) is not kept in Trav: live only during this round, it
     // stays out of the registers held across the streaming kernel's shading code
     const f3 inv = mk(rcp_exact(t.ld.x), rcp_exact(t.ld.y), rcp_exact(t.ld.z));
-#if HG_PHASE_DETAIL == 3
-    uint64_t tp = kp.counters ? wave_clock() : 0;
-#endif
     const uint64_t act_mask = wave_ballot(act);  // act is fixed for the round
     const uint32_t dt = kp.descent_t;
     // lanes at an inner node (HG_NONE has the leaf bit): the wave descends while more than dt of them are left, or
@@ -1143,49 +799,9 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
     uint64_t dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     while (dm != 0ull && (uint32_t(__builtin_popcountll(dm)) > dt || dm == act_mask)) {
         c.node_rounds += wave_once();
-#if HG_COHERENCE_STATS  // analysis builds: distinct node records among the loading lanes, into shade_detail[0..3]
-        if (kp.counters) {  // buckets: 1-4 / 5-16 / 17-32 / more than 32 distinct records per node round
-            uint64_t m = dm;
-            uint32_t k = 0;
-            while (m != 0ull) {
-                const uint32_t first = uint32_t(__builtin_amdgcn_readlane(int(t.node), int(__builtin_ctzll(m))));
-                m &= ~wave_ballot(t.node == first);
-                ++k;
-            }
-            const int slot = k <= 4u ? 11 : k <= 16u ? 12 : k <= 32u ? 13 : 14;
-            if (int(threadIdx.x & 63u) == __ffsll((unsigned long long)__ballot(1)) - 1)
-                atomicAdd(kp.counters + slot, 1ull);
-        }
-#endif
-#if (HG_QUAD_FETCH || HG_NODE_DEDUP) && !HG_NODE_CACHE
-        const bool want = act && int32_t(t.node) >= 0;
-        NodePair np;
-#if HG_NODE_DEDUP
-        const bool coop = wave_node_fetch(kp, want, t.node, np);
-#else
-        const bool coop = quad_node_fetch(kp, want, t.node, np.q0, np.q1, np.q2, np.q3);
-#endif
-        if (want) {
-            if (!coop) np = node_pair(kp, t.node);
-#else
         if (act && int32_t(t.node) >= 0) {
-#endif
-#if (HG_QUAD_FETCH || HG_NODE_DEDUP) && !HG_NODE_CACHE
-#elif HG_NODE_CACHE
-            // the BLAS tops (records [0, hot_records), hot_prefix) come from the wave's LDS copy
-            const NodePair np = t.node < kp.hot_records
-                                    ? node_pair_at(reinterpret_cast<const float4*>(hg_lds_stack + HG_STREAM_CACHE_ROW * 64u) +
-                                                   4u * t.node)
-                                    : node_pair(kp, t.node);
-#else
             const NodePair np = node_pair(kp, t.node);
-#endif
             const uint32_t refA = pair_ref_a(np), refB = pair_ref_b(np);
-#if HG_NODE_PREFETCH
-            // after all four loads have landed (vmcnt retires in order: a wait for a later load would include it)
-            asm volatile("" : : "v"(np.q0.w), "v"(np.q1.w), "v"(np.q2.z), "v"(np.q3.y));
-            node_prefetch(kp, refA, refB);
-#endif
             float dA, dB;
             pair_dist(np, t.lo, inv, dA, dB);
             c.aabb += 2;
@@ -1198,51 +814,30 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         }
         dm = act_mask & wave_ballot(int32_t(t.node) >= 0);
     }
-#if HG_PHASE_DETAIL == 3
-    if (kp.counters) tp = phase_mark(kp, 11, tp);
-#endif
-    bool seq_leaf = true;  // the leaf's triangles tested by the lane itself, in order
-#if HG_LEAF_DIST
-    {
-        const bool at_leaf = act && t.node != HG_NONE && (t.node & HG_LEAF_BIT);
-        uint32_t first = 0u, n = 0u;
-        if (at_leaf) {
-            const uint2 lr = leaf_range(kp, t.node);
-            first = lr.x;
-            n = lr.y;
-        }
-        // distribute only when the longest leaf would take enough sequential rounds to pay for the exchange
-        if (HG_LEAF_DIST_MIN <= 1 || uint32_t(__builtin_amdgcn_readlane(int(wave_incl_max(n)), 63)) >= HG_LEAF_DIST_MIN) {
-            if (leaf_dist(kp, LeafRay{t.lo, t.ld, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, t.mi}, c,
-                          ls, first, n)) {
-                if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
-                seq_leaf = false;
-            }
-        }
+    // Distributed leaf test (HG_LEAF_DIST of rounds 1-4: C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % ->
+    // 70 %, tools/sweeps/sweep52.txt); check builds fall back to the lane's own sequential loop under a partial EXEC
+    const bool at_leaf = act && t.node != HG_NONE && (t.node & HG_LEAF_BIT);
+    uint32_t first = 0u, n = 0u;
+    if (at_leaf) {
+        const uint2 lr = leaf_range(kp, t.node);
+        first = lr.x;
+        n = lr.y;
     }
-#else
-    (void)ls;
-#endif
-    if (seq_leaf && act && t.node != HG_NONE && (t.node & HG_LEAF_BIT)) {  // :404-420
+    if (leaf_dist(kp, LeafRay{t.lo, t.ld, t.best_t, t.best_u, t.best_v, t.best_tri, t.best_mesh, t.mi}, c, ls, first,
+                  n)) {
+        if (at_leaf) t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
+    } else if (at_leaf) {  // (HG_CHECK_EXEC builds only) :404-420, the next triangle's loads out before this one's test
         const uint2 leaf = leaf_range(kp, t.node);
         const uint32_t end = leaf.x + leaf.y;
-#if HG_STREAM_TRI_PREFETCH
         float4 na, nb;
         float nc;
         tri_load(kp, leaf.x, na, nb, nc);
-#endif
         for (uint32_t ti = leaf.x; ti < end; ++ti) {
             c.tri_rounds += wave_once();
-#if HG_STREAM_TRI_PREFETCH  // the next triangle's loads go out before this one is tested
             const float4 a = na, b = nb;
             const float cz = nc;
             const uint32_t tn = ti + 1 < end ? ti + 1 : ti;
             tri_load(kp, tn, na, nb, nc);
-#else
-            float4 a, b;
-            float cz;
-            tri_load(kp, ti, a, b, cz);
-#endif
             c.tri++;
             float tt, U, V;
             bool front;
@@ -1256,21 +851,12 @@ __device__ __forceinline__ void trav_step(const HgKernelParams& kp, const Ray& r
         }
         t.node = t.sp > 0 ? stk.pop(t.sp) : HG_NONE;
     }
-#if HG_PHASE_DETAIL == 3
-    if (kp.counters) tp = phase_mark(kp, 12, tp);
-#endif
     if (act && t.node == HG_NONE) {
         const uint32_t nm = uint32_t(kp.n_meshes);
         t.mi = next_live_mesh(t.live, t.mi + 1u, nm);
         f3 inv_next;
         if (t.mi < nm) mesh_local_ray<kMeshLds>(kp, ray, t.mi, t.lo, t.ld, inv_next, t.node);
     }
-#if HG_PHASE_DETAIL == 3
-    if (kp.counters) {
-        asm volatile("" : : "v"(t.node), "v"(t.lo.x), "v"(t.ld.x));
-        tp = phase_mark(kp, 13, tp);
-    }
-#endif
 }
 
 // The hit get_ray_intersection returns, from a finished traversal (:452-471 and the sphere pass).
@@ -1649,16 +1235,13 @@ __device__ __forceinline__ float inv_blackman_harris(float x) {
 __device__ Ray camera_ray(const HgKernelParams& kp, const Sampler& smp, float ndcx, float ndcy) {
     float j0, j1;
     f3 ap = mk(0.0f, 0.0f, 0.0f);
-#if HG_PINHOLE_FAST
     // Pinhole (disc radius 0): ap is (+-0, +-0, 0), the zeros' signs those of cos / sin.  Nothing below can see them
     // when the camera translation has no zero component (m[3] + (+-0) = m[3] in xform) and pf has no -0 component:
     // ndcx, ndcy are never -0 (x - 1 rounds an exact 0 to +0), so with vw, vh > 0 screen.x, .y are never -0 either
     // (+0 + -0 = +0; no sum underflows), and normalize / the focal distance > 0 keep the sign.  Then pf - (+-0) = pf,
     // and the focal sample and its sincos are skipped: the same bits.
     if (!(kp.focal_disc_radius == 0.0f && kp.cam[3] != 0.0f && kp.cam[7] != 0.0f && kp.cam[11] != 0.0f &&
-          kp.vw > 0.0f && kp.vh > 0.0f && kp.near_ > 0.0f && kp.focal_dist > 0.0f))
-#endif
-    {
+          kp.vw > 0.0f && kp.vh > 0.0f && kp.near_ > 0.0f && kp.focal_dist > 0.0f)) {
         float fd0, fd1;
         smp.get2(ID_FOCAL, fd0, fd1);
         const float th = (fd0 * 360.0f) * HG_DEG2RAD;

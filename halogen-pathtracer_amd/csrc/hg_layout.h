@@ -11,17 +11,21 @@
 //   node ref       uint32: bit 31 = leaf, bits 0..30 = global BLAS index (= accelerationBufferOffset +
 //                  mesh-relative index).  Decided at upload from triangleCount, so the kernel never has to
 //                  read a node to know what it is.
-//   triangles      36 B per triangle in three streams: tri_a = (v0.xyz, e1.x), tri_b = (e1.yz, e2.xy),
-//                  tri_c = e2.z, where e1 = v1 - v0 and e2 = v2 - v0 are the reference's own first two
-//                  subtractions (:312-313) done once on the host with the same IEEE operation.
+//   triangles      36 B per triangle, packed (v0.xyz, e1.xyz, e2.xyz), where e1 = v1 - v0 and e2 = v2 - v0 are the
+//                  reference's own first two subtractions (:312-313) done once on the host with the same IEEE
+//                  operation; a leaf's triangles sit on 2-3 cache lines.
 //   normals        48 B per triangle (n0, n1 - n0, n2 - n0), read once per accepted hit.
-//   meshes         80 B per mesh: full worldToLocal (16 floats, Unity column-major), root ref, triangle
-//                  offset, material index.
+//   meshes         144 B per mesh (HgDevMesh): full worldToLocal (16 floats, Unity column-major), root ref,
+//                  triangle offset, material index, the exact-cull boxes.
 //   spheres        48 B: (centre, radius), (cornerA, material bits), (cornerB, 0).
 //   materials      80 B: albedo; (specular.rgb, metallic); (emissive.rgb*intensity, roughness);
 //                  (absorption.xyz, ior); (priority, medium id, roughness^2, 0).
 //   accumulation   float4 per pixel, TILE-MAJOR: 8x8 tiles of 1 KiB, local tile t holds global tile
 //                  rank + t*n_ranks, pixel (lx,ly) at lx + 8*ly — one wave writes one contiguous KiB.
+//
+// The measured-and-rejected experiments of rounds 1-4 (wavefront pipeline, path pool, LDS node cache, quad /
+// deduplicated node fetch, ray sort, path migration, packed-pair and stream triangle layouts, ...) were removed from
+// the sources in round 5; their designs and numbers stay in DESIGN.md section 10 and in git history.
 #pragma once
 #include <stdint.h>
 
@@ -33,15 +37,8 @@
 #define HG_LEAF_PAYLOAD ((1u << HG_LEAF_CNT_SHIFT) - 1u)
 #define HG_TILE 8
 #define HG_MAX_CUBE_MIPS 16
-#define HG_LDS_STACK 16  // wavefront trace: traversal stack entries per lane kept in LDS
 #define HG_REGEN_MAX_BOUNCES 250  // regenerating megakernel: byte-packed bounce counters (larger: lockstep kernel)
 #define HG_REGEN_MAX_CHUNK 65535  // regenerating megakernel: frames per launch and spp limit (16-bit fields)
-#ifndef HG_POOL_TILES
-#define HG_POOL_TILES 4  // path-pool kernel: 8x8 tiles (64 paths each) per wave
-#endif
-#ifndef HG_POOL_WAVES
-#define HG_POOL_WAVES 6  // path-pool kernel: waves/SIMD target
-#endif
 #ifndef HG_LOCK_WAVES
 #define HG_LOCK_WAVES 4  // lockstep megakernel (debug views, large-maxBounces fallback): waves/SIMD target
 #endif
@@ -49,17 +46,11 @@
 #define HG_MEGA_WAVES 6  // regenerating megakernel: waves/SIMD target
 #endif
 #ifndef HG_STREAM_WAVES
-#define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~120 VGPRs)
+#define HG_STREAM_WAVES 5  // streaming kernel: waves/SIMD target (its resumable traversal state needs ~96 VGPRs)
 #endif
 #ifndef HG_STREAM_TMIN
 #define HG_STREAM_TMIN 16  // streaming kernel: shade once at most this many lanes are still traversing (12 before the
                            // item scheduling, tools/sweeps/sweep54.txt; 16 with it, +1.1 %, tools/sweep_r02_ac.txt)
-#endif
-#ifndef HG_RCP_NORMALIZE
-#define HG_RCP_NORMALIZE 0  // normalize via rcp_exact(sqrt) instead of the IEEE division (same bits)
-#endif
-#ifndef HG_BRANCHLESS_DESCENT
-#define HG_BRANCHLESS_DESCENT 0  // descent: select-based near/far/pop decision
 #endif
 #ifndef HG_DESCENT_T
 #define HG_DESCENT_T 3  // deep scenes (BLAS depth > HG_DESCENT_DEEP): leave the descent loop at <= T descending lanes
@@ -80,78 +71,18 @@
 #ifndef HG_DESCENT_DEEP
 #define HG_DESCENT_DEEP 16
 #endif
-#ifndef HG_TRAV_IFIF
-#define HG_TRAV_IFIF 0  // traversal rounds: 1 = if-if (node step or leaf per round), 0 = while-while
-#endif
-#ifndef HG_LANE_MESHES
-#define HG_LANE_MESHES 1  // traversal: per-lane mesh cursor (1) or wave-uniform mesh loop (0)
-#endif
-#ifndef HG_XCD_REMAP
-#define HG_XCD_REMAP 0  // contiguous tile band per XCD: measured 24% SLOWER (static per-XCD imbalance), off
-#endif
-#ifndef HG_TRI_PREFETCH
-#define HG_TRI_PREFETCH 0  // leaf loop: issue the next triangle's loads before testing the current one
-#endif                     // (regen: C2 -13 %, C5 -16 %: the registers spill; tools/sweeps/sweep47.txt)
-#ifndef HG_STREAM_TRI_PREFETCH
-#define HG_STREAM_TRI_PREFETCH 1  // the same in the streaming kernel's leaf loop: C3 +3 % at no register cost
-#endif
-#ifndef HG_LEAF_DIST
-#define HG_LEAF_DIST 1  // streaming traversal: a round's (ray, triangle) pairs dealt over all 64 lanes, LDS min-reduce
-#endif                   // (C3 2013 -> 2074 Mpaths/s, leaf-loop lane utilisation 25 % -> 70 %; tools/sweeps/sweep52.txt)
-#ifndef HG_PINHOLE_FAST
-#define HG_PINHOLE_FAST 1  // camera_ray skips the focal-disc sample when the disc radius is 0 (same bits, hg_device.h)
-#endif
-#ifndef HG_LEAF_DIST_MIN
-#define HG_LEAF_DIST_MIN 1  // ... only when the wave's longest leaf has at least this many triangles (1: always;
-#endif                      // 2 / 3 measured 2066 / 2063)
-#ifndef HG_SHADE_PRIO
-#define HG_SHADE_PRIO 2  // streaming kernel wave priority (s_setprio): 1 = raised while shading, k >= 2 = raised to
-#endif                    // k-1 while traversing (C3 2,097 -> 2,111, k = 2/3/4 alike; tools/sweeps/sweep67-68.txt)
-#ifndef HG_REGEN_PRIO
-#define HG_REGEN_PRIO 1  // regenerating kernel: wave priority raised during get_ray_intersection (C2 +1 %, C5 +2 %,
-#endif                   // tools/sweeps/sweep69.txt)
-#ifndef HG_NODE_PREFETCH
-#define HG_NODE_PREFETCH 0  // streaming traversal: prefetch the children's record line (global_load_lds)
-#endif
-#ifndef HG_TRI_AOS
-#define HG_TRI_AOS 1  // triangles as packed 36-B records (v0, e1, e2; tri_load's three loads on one record) instead of
-#endif            // the three streams tri_a / tri_b / tri_c (a leaf's triangles on fewer cache lines)
-#ifndef HG_PAIR_SOA
-#define HG_PAIR_SOA 0  // child-pair records coordinate by coordinate, A and B side by side: packed-FP32 box tests
-#endif             // (node_pair / pair_dist in hg_device.h; the record writer in hg_runtime.hip)
-#ifndef HG_FC_NT
-#define HG_FC_NT 1  // frame-colour stores (trace) and loads (blend) with the non-temporal hint (+0.2..0.6 %, sweep_r03_n)
-#endif
-#ifndef HG_QUAD_FETCH
-#define HG_QUAD_FETCH 0  // streaming traversal node fetch: 1 = quad-cooperative (each quad loads its 4 lanes' records
-#endif                   // whole, one record per round, then a DPP transpose), 2 = cooperative only when >= HG_QUAD_MIN
-#ifndef HG_QUAD_MIN      // of the 16 quads need 2+ distinct records (DESIGN.md §10 lever 4)
-#define HG_QUAD_MIN 8
-#endif
+// Wave priorities (s_setprio): the streaming kernel's waves run at 1 while traversing (traversal waits on memory: its
+// waves issue first) and 0 while shading (C3 2,097 -> 2,111, tools/sweeps/sweep67-68.txt); the regenerating kernel's
+// at 1 during get_ray_intersection (C2 +1 %, C5 +2 %, tools/sweeps/sweep69.txt).
+#define HG_TRAVERSE_PRIO 1
 #ifndef HG_TILE_ORDER
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif
-#ifndef HG_UNIT_TILE_MAJOR
-#define HG_UNIT_TILE_MAJOR 1  // cost order: a tile's frame chunks on consecutive waves (hg_mega.hip wave_unit; tools/sweeps/sweep81.txt)
-#endif
-#ifndef HG_PHASE_DETAIL
-#define HG_PHASE_DETAIL 0  // analysis builds: streaming kernel's shading sub-phase clocks in counter slots 11..14
-#endif
-// (HG_LDS_ACC, the round-2 LDS accumulator of unsplit per-pixel-lane launches, is gone: the item scheduling replaced
-// those launches.  A 1-frame launch now blends straight into the accumulator, hg_mega.hip.)
 #ifndef HG_ORDER_MIN_FRAMES
 #define HG_ORDER_MIN_FRAMES 16  // hg_render re-sorts the tile order once at least this many frames of costs were recorded
 #endif                          // since the last sort (64-frame launches: every launch; 1-frame launches: every 16th)
-#ifndef HG_NODE_CACHE
-#define HG_NODE_CACHE 0  // streaming kernel: the top records of every BLAS (BFS) copied into LDS per wave (records,
-#endif                   // a multiple of 4: 4 records = one 64-lane LDS row)
-#define HG_STREAM_CACHE_ROW 13  // its first LDS row (after the per-lane state rows, hg_mega.hip kRowStack)
-#ifndef HG_MESH_LDS
-#define HG_MESH_LDS 1  // streaming kernel: every mesh's world->local matrix and header (80 B) in the wave's LDS
-#endif                 // when they fit (hg_mesh_lds_fits): the per-lane mesh switch reads LDS, not global memory
-#ifndef HG_STREAM_LDS_PAD
-#define HG_STREAM_LDS_PAD 0  // analysis builds: extra LDS bytes per streaming workgroup (occupancy experiments)
-#endif
+// Every mesh's world->local matrix and header (80 B) in the wave's LDS when they fit (mesh_lds_bytes): the per-lane
+// mesh switch reads LDS, not global memory
 #define HG_MESH_LDS_F4 5  // float4 per cached mesh record: w2l columns 0-3, header (root, tri offset, material, cull)
 // Bytes of LDS per one-wave workgroup that still keep 20 waves (5 per SIMD) on a CU.  Measured, not derived from
 // 160 KiB / 20: 7,424 and 7,472 B run at full occupancy, 7,936 / 7,984 / 8,192 B lose 8-12 % (one wave fewer per
@@ -164,14 +95,6 @@
 // reserve; 0 keeps its mesh records in global memory
 #define HG_REGEN_LDS_BUDGET 6144
 #endif
-// (HG_STREAM_ITEMS, lanes owning pixels instead of taking (pixel, frame) items, is gone: the streaming kernel always takes
-// items and stores frame colours; hg_mega.hip)
-#ifndef HG_FC_SLOT_MAJOR
-#define HG_FC_SLOT_MAJOR 1  // frame colours stored [slot][frame] (a pixel's frames contiguous) instead of [frame][slot]
-#endif
-#ifndef HG_DIAG_NO_FC
-#define HG_DIAG_NO_FC 0  // analysis builds: the streaming kernel skips its frame-colour stores (wrong images; WRITE_SIZE split)
-#endif
 #ifndef HG_COALESCE
 #define HG_COALESCE 32  // default HG_OPT_COALESCE: frames of consecutive hg_render calls held for one launch
 #endif
@@ -180,47 +103,23 @@
 #endif                    // order.  1-frame launches, C3, all waves per launch: 2 streams 1,970, 3: 2,143, 4: 2,265,
                           // 6: 2,242, 8: 2,302 Mpaths/s; with HG_QUEUE_WAVES_DIV 6 and 8 streams 2,745, with 8 and 10 / 12
                           // streams 2,808 / 2,790 (tools/sweeps/sweep_r03_u/v/y/z/aa; streams 3+ on hardware queues of
-                          // their own, HG_LANE_STREAMS).  Round 4 (queue heads reset in-kernel, small sort), streams /
-                          // divisor 8/6 2,779-2,793, 12/8 2,874-2,878, 12/12 2,748-2,753, 16/12 2,893-2,908, 16/16
-                          // 2,800-2,808 (tools/sweeps/sweep_r04_a.txt): 12/8, +3 % for four more queues per context
+                          // their own).  Round 4 (queue heads reset in-kernel, small sort), streams / divisor 8/6
+                          // 2,779-2,793, 12/8 2,874-2,878, 12/12 2,748-2,753, 16/12 2,893-2,908, 16/16 2,800-2,808
+                          // (tools/sweeps/sweep_r04_a.txt): 12/8, +3 % for four more queues per context
 #ifndef HG_TRACE_LANES_BIG
 #define HG_TRACE_LANES_BIG 2  // of those, the ones chunks of more than HG_QUEUE_MAX_FRAMES frames take in turn (a third
 #endif                        // 64-frame launch beside two others: C3 -1.5 %)
-#ifndef HG_LANE_STREAMS
-// How the trace streams are created.  HIP spreads plain streams over a pool of GPU_MAX_HW_QUEUES (default 4) hardware
-// queues shared by every stream of the process, and two streams on one queue run their launches one after the other:
-// a third plain trace stream cost 1-frame launches 16 % (1,663 vs 1,970; 2,111 with GPU_MAX_HW_QUEUES=8).  A stream
-// created with a CU mask gets a hardware queue of its own.  0: plain, 1: all with an all-CU mask, 2: all with the
-// greatest stream priority (also a queue of its own: 2,121 at 3 streams), 3: plain for the first HG_TRACE_LANES_BIG
-// (non-blocking, as before), an all-CU mask for the others (4 streams: 2,266 vs 2,260 all masked; batched equal).
-#define HG_LANE_STREAMS 3
-#endif
+// Trace streams: HIP spreads plain streams over a pool of GPU_MAX_HW_QUEUES (default 4) hardware queues shared by every
+// stream of the process, and two streams on one queue run their launches one after the other (a third plain trace
+// stream cost 1-frame launches 16 %: 1,663 vs 1,970).  A stream created with a CU mask gets a hardware queue of its
+// own: the first HG_TRACE_LANES_BIG trace streams are plain and non-blocking, the others (and the render server's and
+// the side copy stream) carry an all-CU mask (create_lane_stream, hg_runtime.hip).
 #ifndef HG_QUEUE_WAVES_DIV
 #define HG_QUEUE_WAVES_DIV 8  // queue launches beside >= 2 other traces in flight: at most this many times fewer persistent
 #endif                        // waves than resident slots (hg_render; C3 1-frame launches, 8 streams: 1 2,265 -> 6 2,745;
                               // 12 streams: 8 2,874-2,878, 12 2,748-2,753)
 #ifndef HG_READBACK_SIDE
 #define HG_READBACK_SIDE 0  // default HG_OPT_READBACK_STREAM (display copies on a side stream)
-#endif
-#ifndef HG_NODE_DEDUP
-#define HG_NODE_DEDUP 0  // streaming traversal: wave-level deduplicated node fetch (hg_device.h wave_node_fetch)
-#endif
-#ifndef HG_RB_OWN_QUEUE
-#define HG_RB_OWN_QUEUE 1  // HG_OPT_READBACK_STREAM's copy stream CU-masked, on a hardware queue of its own: a plain one shares
-#endif                     // a queue with a trace lane and waits behind its traces (depth 2: 1,285 -> 1,642; sweep_r04_rbq)
-#ifndef HG_MAT_SCALAR
-#define HG_MAT_SCALAR 0  // A/B: a material record the wave's shading lanes share is read with scalar loads
-#endif
-#ifndef HG_DRAIN_PRIO
-#define HG_DRAIN_PRIO 0  // A/B: streaming waves at priority 2 / 1 (traversal / shading), queue waves past the queue's end at 0
-#endif
-#ifndef HG_WAVE_TIMELINE
-#define HG_WAVE_TIMELINE 0  // analysis builds: queue waves record their start / queue-dry / end times (tools/wave_timeline.py)
-#endif
-#define HG_TIMELINE_LAUNCHES 64  // ... for the last this many queue launches, at most HG_TIMELINE_WAVES waves each
-#define HG_TIMELINE_WAVES 8192
-#ifndef HG_COHERENCE_STATS
-#define HG_COHERENCE_STATS 0  // analysis builds: histogram of distinct node records per descent round (hg_device.h)
 #endif
 #ifndef HG_WAVE_UNITS_MAX
 #define HG_WAVE_UNITS_MAX 1     // streaming launches without the queue: at most this many tiles per wave (automatic)
@@ -238,38 +137,22 @@
 // The queue of a kQueue launch: 8 unit heads, 128 B apart (words 32 h), then the count of waves that have left (its own
 // 128-B line): the last wave out zeroes them for the next launch (the runtime zeroes the buffer once, at allocation)
 #define HG_QUEUE_DONE_WORD 256u
-#ifndef HG_QUEUE_DONE_RELAXED
-#define HG_QUEUE_DONE_RELAXED 0
-#endif
-#ifndef HG_PATH_MIGRATE
-#define HG_PATH_MIGRATE 0  // kQueue drain: waves left with few paths hand them to other waves at ray boundaries (§4.6)
-#endif
-#ifndef HG_MIG_KERNEL
-#define HG_MIG_KERNEL HG_PATH_MIGRATE  // (A/B: 0 keeps the runtime side only)
-#endif
-#ifndef HG_MIG_RETIRE
-#define HG_MIG_RETIRE 16  // ... a queue-dry wave with at most this many paths in flight retires (exports, then leaves)
-#endif
-#ifndef HG_MIG_POLL_IDLE
-#define HG_MIG_POLL_IDLE 16  // ... a dry wave tests the pool (a device-coherent load) with at least this many idle lanes
-#endif
-#ifndef HG_MIG_KEEP_SHIFT
-#define HG_MIG_KEEP_SHIFT 1  // ... while at least gridDim >> this many of the launch's waves stay (all retiring: 3x slower)
-#endif
-// Path migration words of the queue buffer (each on its own 128-B line): the 64-bit (waves gone | exporting waves
-// << 32) state, the pool's (reserved | taken << 32) counts; then the pool, one 128-B record per exported path
-// (at most 64 per wave of the launch)
-#define HG_MIG_STATE_WORD 288u
-#define HG_MIG_POOL_WORD 320u
-#define HG_MIG_POOL_BYTE 2048u
 #define HG_QUEUE_BYTES (9u * 128u)
-#define HG_QUEUE_BYTES_MIG(slots) (size_t(HG_MIG_POOL_BYTE) + size_t(slots) * 64u * 128u)
-#ifndef HG_ITEMS_PIXEL_MAJOR
-#define HG_ITEMS_PIXEL_MAJOR 1  // items k -> (pixel k / frames, frame k % frames): a wave's lanes trace one pixel's frames
-                                // (with HG_FC_SLOT_MAJOR: C3 +0.4 %, C2 +0.5 %, C5 -0.4 %; tools/sweeps/sweep_r02_be/bf)
+// The render server's control block (kp.queue of a server launch, zeroed before it): the 8 unit heads as above, then on
+// lines of their own the device mirror of the host's post word (u64, raised by atomic max by whichever wave reads the
+// host word) and the host-poll ticket (u64 s_memrealtime: one wave reads the host word per HG_SV_POLL_TICKS).
+#define HG_SV_MIRROR_WORD 288u
+#define HG_SV_TICKET_WORD 320u
+#define HG_SV_CTL_BYTES (11u * 128u)
+#ifndef HG_SV_POLL_TICKS
+#define HG_SV_POLL_TICKS 50u  // 0.5 us between reads of the host word over PCIe, for the whole GPU
 #endif
+#ifndef HG_SV_RING
+#define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most
+#endif
+#define HG_SV_STOP (1ull << 32)  // the post word's stop flag (posted frames in the low 32 bits)
 #ifndef HG_REGEN_ITEMS
-#define HG_REGEN_ITEMS 1  // regenerating kernel: the same (pixel, frame) item scheduling (HG_STREAM_ITEMS)
+#define HG_REGEN_ITEMS 1  // regenerating kernel: (pixel, frame) item scheduling (0: the A/B build of make noitems)
 #endif
 #ifndef HG_STREAM_MIN_MESHES
 #define HG_STREAM_MIN_MESHES 4  // HG_KERNEL_AUTO: the streaming kernel from this many meshes on (or for a deep BLAS)
@@ -321,8 +204,10 @@ struct HgKernelParams {
     // [k*n_frames/split, (k+1)*n_frames/split) into frame_color (fc_index); hg_blend_frames then applies the
     // accumulation blend in frame order.  frame_split == 1: the kernel blends into acc itself.
     int32_t frame_split;
-    float4* __restrict__ frame_color;
-    float4* __restrict__ pool;  // path-pool kernel: per-wave path slots (hg_pool.hip)
+    float4* __restrict__ frame_color;  // render server: a ring of sv_ring frames, frame k at [(k & (sv_ring-1)) * slots]
+    // render server (kServer): per ring slot a completion count on its own 128-B line (word 32 s), advanced by
+    // n_local_tiles for every frame of that slot; the context stream's gate waits for it (hg_server_gate)
+    uint32_t* __restrict__ frames_done;
     // cost-ordered dispatch (regen / stream kernels): wave w traces local tile tile_order[w % n_local_tiles] (null:
     // tile w % n_local_tiles) and adds its wave-clock cost to tile_cost[tile] (null: not recorded).  Any permutation
     // gives the same image: tiles are independent and each tile's frames keep their order.
@@ -335,16 +220,18 @@ struct HgKernelParams {
     // streaming launches without the queue and without a frame split: each wave traces wave_units consecutive units
     // of the cost order (1: one tile per wave), its lanes taking their items one after another (UnitItems)
     uint32_t wave_units;
-    // analysis builds (HG_WAVE_TIMELINE=1), queue launches: per wave (start, queue dry, end, items) in 100-MHz ticks
-    unsigned long long* __restrict__ timeline;
+    // render server: the host's post word in pinned host memory (frames posted | stop << 32), read by the device
+    const unsigned long long* __restrict__ sv_post;
+    uint32_t sv_ring;        // colour ring slots (a power of two)
+    uint32_t sv_frames_cap;  // frames the server may trace in its lifetime (n_local_tiles * frames < 2^31)
+    uint32_t sv_idle_ticks;  // a wave idle this long (100-MHz s_memrealtime ticks) with nothing posted leaves
+    uint32_t sv_div_magic, sv_div_shift;  // unit -> frame: u / n_local_tiles = umulhi(u, magic) >> shift (u < 2^31)
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
-    uint32_t hot_records;  // HG_NODE_CACHE: node records [0, hot_records) are served from the wave's LDS copy
-    uint32_t mesh_lds_word;  // HG_MESH_LDS: LDS word where the wave's copy of the mesh records starts
+    uint32_t mesh_lds_word;  // the mesh records' LDS copy starts at this word (mesh_lds_bytes, hg_mega.hip)
     uint32_t descent_t;    // relaxed while-while threshold (hg_device.h isect_meshes), 0 = classic while-while
     uint32_t stream_deep;  // streaming kernel: the deep-BLAS shading thresholds (HG_STREAM_TMIN_DEEP / _RESHADE_DEEP)
-    uint32_t refill_min;   // wavefront trace: dequeue only when at least this many lanes are idle (or all are)
     uint32_t* __restrict__ spill;  // per-lane traversal stack entries beyond the LDS part (rarely touched)
     uint32_t spill_stride;          // = threads of the launch grid
     // cubemap
@@ -356,29 +243,13 @@ struct HgKernelParams {
     const float4* __restrict__ materials;
     const float4* __restrict__ nodes;
     const uint2* __restrict__ leaves;
-    const float4* __restrict__ tri_a;
-    const float4* __restrict__ tri_b;
-    const float* __restrict__ tri_c;
+    const float* __restrict__ tris;  // 9 floats per triangle: v0, e1, e2
     const float4* __restrict__ normals;
     const float4* __restrict__ cube;
     // outputs
     float4* __restrict__ acc;
     unsigned long long* __restrict__ counters;  // 32 x u64: 0-6 hg_counters' first 7 fields, 7-15 wave-level
                                                 // rounds / clocks, 16 primary misses (hg_runtime.hip hg_get_counters)
-
-    // wavefront pipeline state (hg_wavefront.hip), SoA, one entry per local pixel slot
-    // (slot = local_tile*64 + lane, the same index as the tile-major accumulation buffer)
-    uint32_t n_slots;
-    float4* __restrict__ p_o;    // ray origin xyz, accumulated roughness (trace_ray's accumulatedRoughnes)
-    float4* __restrict__ p_d;    // ray direction xyz
-    float4* __restrict__ p_thr;  // lightAttenuation xyz
-    float4* __restrict__ p_col;  // accumulatedColor of the current sample xyz
-    float4* __restrict__ p_sum;  // RayColor: sum over the samples of the current frame
-    uint4* __restrict__ p_st;    // bounceTypes[0..2], rayInteractions
-    uint4* __restrict__ p_st2;   // SobolDimensionOffset, sample index, frame index, medium stack pointer
-    uint2* __restrict__ p_ms;    // medium stack: 8 material indices, one byte each
-    float4* __restrict__ h_tuvo; // hit: t, barycentric u, v, orientation
-    uint2* __restrict__ h_id;    // hit: primitive (triangle index | sphere index + HG_SPHERE_BIT | HG_NONE), mesh
 };
 
 #define HG_NONE 0xFFFFFFFFu

@@ -16,7 +16,7 @@ using namespace hgd;
 template <bool kCounters, bool kDebug>
 __global__ __launch_bounds__(256, HG_LOCK_WAVES) void hg_trace_kernel(const HgKernelParams kp) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int local_tile = int(xcd_block(blockIdx.x, gridDim.x)) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
+    const int local_tile = int(blockIdx.x) * int(blockDim.x >> 6) + int(threadIdx.x >> 6);
     const int gtile = kp.rank + local_tile * kp.n_ranks;
     const uint32_t px = uint32_t(gtile % kp.tiles_x) * HG_TILE + (lane & 7u);
     const uint32_t py = uint32_t(gtile / kp.tiles_x) * HG_TILE + (lane >> 3);
@@ -93,36 +93,27 @@ constexpr uint32_t kStreamLdsState = 10;
 // Streaming kernel LDS rows (one wave per workgroup, RowVec / RowStack): throughput 0-2, path colour 3-5, sample sum
 // 6-8, the distributed leaf test 10-12, the traversal stack from row 13.
 constexpr uint32_t kRowThr = 0, kRowCol = 3, kRowSum = 6, kRowLeaf = kStreamLdsState;
-[[maybe_unused]] constexpr uint32_t kRowSort = 9;  // HG_RAY_SORT builds: the lane-permutation scratch row
-constexpr uint32_t kRowCache = kRowLeaf + 3, kRowStack = kRowCache + HG_NODE_CACHE / 4;  // node cache rows, stack
-static_assert(kRowCache == HG_STREAM_CACHE_ROW && HG_NODE_CACHE % 4 == 0, "stream LDS rows");
+constexpr uint32_t kRowStack = kRowLeaf + kLeafShareWords;
 constexpr uint32_t kRegenRowStack = kRegenLdsState;  // regenerating kernel: rows 0-8 as above, the stack from row 9
 
 // Cost-ordered dispatch (HgKernelParams::tile_order): the wave's tile, read through the scalar cache (the order is
 // written by hg_order_tiles before this launch and never during it).
 __device__ __forceinline__ int ordered_tile(const HgKernelParams& kp, uint32_t w) {
     if (!kp.tile_order) return int(w);
-#if HG_TILE_ORDER_SCALAR
-    typedef const __attribute__((address_space(4))) uint32_t* cu32p;
-    return int(((cu32p)(uintptr_t)kp.tile_order)[__builtin_amdgcn_readfirstlane(w)]);
-#else
     return int(kp.tile_order[w]);
-#endif
 }
 // The wave's work unit (tile, frame chunk).  Tile-index order: chunk-major (wave w: tile w mod tiles, chunk
-// w / tiles).  Cost order with HG_UNIT_TILE_MAJOR: tile-major (wave w: tile order[w / split], chunk w mod split), so
-// a tile's chunks run side by side and the most expensive tiles' chunks all start first.  Waves past the last unit
-// get chunk = split (no work).
+// w / tiles).  Cost order: tile-major (wave w: tile order[w / split], chunk w mod split), so a tile's chunks run side by
+// side and the most expensive tiles' chunks all start first (tools/sweeps/sweep81.txt).  Waves past the last unit get
+// chunk = split (no work).
 __device__ __forceinline__ void wave_unit(const HgKernelParams& kp, uint32_t gw, uint32_t nlt, uint32_t split,
                                           int& tile, uint32_t& chunk) {
-#if HG_UNIT_TILE_MAJOR
     if (kp.tile_order) {
         const uint32_t w = gw / split;
         tile = w < nlt ? ordered_tile(kp, w) : 0;
         chunk = w < nlt ? gw % split : split;
         return;
     }
-#endif
     tile = ordered_tile(kp, gw % nlt);
     chunk = gw / nlt;
 }
@@ -165,14 +156,8 @@ __device__ __forceinline__ f3 sample_mean(const HgKernelParams& kp, f3 sum) {
 __shared__ uint32_t hg_next_item;  // items of the wave's tile handed out so far (one wave per workgroup)
 struct TileItems {
     uint32_t tx0, ty0, tw, nv, n_items, f_begin;  // wave-uniform (scalar registers)
-#if HG_ITEMS_PIXEL_MAJOR
     uint32_t nf;  // frames of the chunk
-#endif
-    __device__ TileItems() : tx0(0), ty0(0), tw(0), nv(0), n_items(0), f_begin(0) {  // unused (kQueue kernels)
-#if HG_ITEMS_PIXEL_MAJOR
-        nf = 1u;
-#endif
-    }
+    __device__ TileItems() : tx0(0), ty0(0), tw(0), nv(0), n_items(0), f_begin(0), nf(1u) {}  // unused
     __device__ TileItems(const HgKernelParams& kp, int local_tile, bool valid, uint32_t fb, uint32_t fe, uint32_t lane) {
         const int g = __builtin_amdgcn_readfirstlane(kp.rank + local_tile * kp.n_ranks);
         tx0 = uint32_t(g % kp.tiles_x) * HG_TILE;
@@ -182,17 +167,14 @@ struct TileItems {
         nv = tw * th;
         n_items = __builtin_amdgcn_readfirstlane(valid && fe > fb ? nv * (fe - fb) : 0u);
         f_begin = fb;
-#if HG_ITEMS_PIXEL_MAJOR
         nf = __builtin_amdgcn_readfirstlane(fe > fb ? fe - fb : 1u);
-#endif
         if (lane == 0) hg_next_item = 64u;  // lane l starts with item l
         wave_lds_sync();
     }
-    // item k -> its pixel within the tile (x + 8 y) and its frame: shifts for a whole tile, divisions at the edge
+    // item k -> valid pixel k / nf (its pixel within the tile, x + 8 y) and frame k mod nf: a wave's lanes trace one
+    // pixel's frames (with the [slot][frame] colours: C3 +0.4 %, C2 +0.5 %, C5 -0.4 %; tools/sweeps/sweep_r02_be/bf)
     __device__ __forceinline__ void get(uint32_t k, uint32_t& pix, uint32_t& frame) const {
-        uint32_t q;
-#if HG_ITEMS_PIXEL_MAJOR  // item k -> valid pixel k / nf, frame k mod nf (a wave's lanes on one pixel's frames)
-        uint32_t i;
+        uint32_t q, i;
         if ((nf & (nf - 1u)) == 0u) {
             const uint32_t lg = uint32_t(__builtin_ctz(nf));
             i = k >> lg;
@@ -202,17 +184,6 @@ struct TileItems {
             q = k - i * nf;
         }
         pix = nv == 64u ? i : (i % tw) + 8u * (i / tw);
-        frame = f_begin + q;
-        return;
-#endif
-        if (nv == 64u) {
-            pix = k & 63u;
-            q = k >> 6;
-        } else {
-            q = k / nv;
-            const uint32_t i = k - q * nv;
-            pix = (i % tw) + 8u * (i / tw);
-        }
         frame = f_begin + q;
     }
     // Called by exactly the lanes that need an item (the active lanes): they take the next items in lane order.  The
@@ -495,7 +466,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
     }
     // wave -> (tile, frame chunk): with frame_split == 1 the wave index is the tile
     // one wave per workgroup (launched with 64 threads): wave = workgroup; LDS rows as the streaming kernel's
-    const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t gw = blockIdx.x;
     const uint32_t nlt = uint32_t(kp.n_local_tiles), split = uint32_t(kp.frame_split);
     int local_tile;
     uint32_t chunk;
@@ -551,13 +522,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
         const bool was_work = work;
         uint64_t t1 = 0;
         if (work) {
-#if HG_REGEN_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
+            __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
             const Hit hit = intersect<kMeshLds>(kp, ray, c, stk);
-#if HG_REGEN_PRIO
             __builtin_amdgcn_s_setprio(0);
-#endif
             if (kCounters) t1 = wave_clock();
             c.shade_rounds += wave_once();
             bool alive = false;
@@ -685,33 +652,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
     }
 }
 
-// Frame-parallel epilogue: acc = acc*(1-w) + c_f*w for f in frame order (AccumulationShader.shader:33), exactly
-// the per-frame blend the kernel does itself when frame_split == 1.
-__global__ __launch_bounds__(256) void hg_blend_frames(float4* __restrict__ acc, const float4* __restrict__ colors,
-                                                       uint32_t n_slots, int32_t n_frames, int32_t first_frame,
-                                                       int32_t accumulate) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_slots) return;
-    float4 a = acc[i];
-    for (int32_t f = 0; f < n_frames; ++f) {
-#if HG_FC_SLOT_MAJOR
-        const float4 c = fc_load(colors + size_t(i) * uint32_t(n_frames) + uint32_t(f));  // fc_index (hg_device.h)
-#else
-        const float4 c = fc_load(colors + size_t(f) * n_slots + i);
-#endif
-        if (accumulate) {
-            const float w = rcp_exact(float(uint32_t(first_frame + f)));
-            const float k = 1.0f - w;
-            a = make_float4(a.x * k + c.x * w, a.y * k + c.y * w, a.z * k + c.z * w, a.w * k + 1.0f * w);
-        } else {
-            a = make_float4(c.x, c.y, c.z, 1.0f);
-        }
-    }
-    acc[i] = a;
-}
-
-#if HG_FC_SLOT_MAJOR
-// The same blend over the [slot][frame] layout: each wave owns 64 slots (a tile) and moves their colours 8 frames at
+// Frame-parallel epilogue: acc = acc*(1-w) + c_f*w for f in frame order (AccumulationShader.shader:33), exactly the
+// per-frame blend the kernels do themselves when they blend in place.
+// Over the [slot][frame] colour layout each wave owns 64 slots (a tile) and moves their colours 8 frames at
 // a time through LDS, so every load instruction reads whole 128-B lines (8 lanes per line: one slot's 8 frames)
 // instead of 64 lanes on 64 lines; then each lane blends its slot's 8 frames in frame order.
 __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ acc, const float4* __restrict__ colors,
@@ -747,7 +690,6 @@ __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ a
     }
     acc[slot0 + lane] = a;
 }
-#endif
 
 // The blend of a launch of few frames (at most HG_QUEUE_MAX_FRAMES): one thread per slot, no LDS, 64-thread groups and
 // few registers.  A 1-frame launch's blend runs while the next launch's persistent trace waves hold the CUs' wave slots
@@ -760,7 +702,7 @@ __global__ __launch_bounds__(64) void hg_blend_frames_lean(float4* __restrict__ 
     if (i >= n_slots) return;
     float4 a = acc[i];
     for (int32_t f = 0; f < n_frames; ++f) {
-        const float4 c = fc_load(colors + fc_slot_frame(i, uint32_t(f), n_slots, uint32_t(n_frames)));
+        const float4 c = fc_load(colors + fc_slot_frame(i, uint32_t(f), uint32_t(n_frames)));
         if (accumulate) {
             const float w = rcp_exact(float(uint32_t(first_frame + f)));
             const float k = 1.0f - w;
@@ -780,19 +722,14 @@ hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) 
                            n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
         return hipGetLastError();
     }
-#if HG_FC_SLOT_MAJOR
     hipLaunchKernelGGL(hg_blend_frames_sm, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc,
                        kp.frame_color, n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
-#else
-    hipLaunchKernelGGL(hg_blend_frames, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc, kp.frame_color,
-                       n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
-#endif
     return hipGetLastError();
 }
 
 // LDS bytes with the mesh records after `base` bytes of rows, or 0 when they do not fit `budget` (or HG_MESH_LDS is off)
 static size_t mesh_lds_bytes(size_t base, int32_t n_meshes, size_t budget) {
-    if (!HG_MESH_LDS || n_meshes <= 0) return 0;
+    if (n_meshes <= 0) return 0;
     const size_t b = base + size_t(n_meshes) * HG_MESH_LDS_F4 * 16u;
     return b <= budget ? b : 0;
 }
@@ -953,118 +890,230 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
     y = ty * HG_TILE + ((slot >> 3) & 7u);
 }
 
-#if HG_MIG_KERNEL
-// Path migration (kQueue).  After the queue runs dry each wave drains: its lanes finish the paths they
-// hold, the idle ones waiting, the wave's slot held until its slowest path ends.  Here a dry wave with at most
-// HG_MIG_RETIRE paths left retires: each of its lanes, when its current ray ends and the path goes on, writes the
-// path's whole state (a ray boundary: no traversal state) to a pool record instead of beginning the ray, and the wave
-// leaves once its lanes are empty; the dry waves that stay take pool records into their idle lanes at the loop top.
-// A path's result does not depend on which lane traces it (the state moves bit for bit).  The 64-bit state word counts
-// the waves gone (retired or left) and, above bit 32, the retired waves still exporting: a wave retires only while
-// another wave of the launch is not gone, and the last one leaves only with no exporter left and the pool empty, so
-// every record is taken.  Records carry slot + 1 as their ready flag (0: not written yet), cleared by the taker.
-__device__ __forceinline__ uint32_t mig_ld(const uint32_t* p) {
+// ---------------------------------------------------------------------------------------------------------------
+// The render server (kServer): the persistent queue waves outlive hg_render calls.  The reference dispatches once per
+// frame (RP:327, RP:406); a launch per frame ends with every wave draining its last paths, its other lanes idle (0.63 ms
+// of a C3 frame's 1.2 ms).  Here one launch serves every frame the host posts while it lives:
+// unit u of the server is (frame k = u / tiles, the tile at cost-order position u mod tiles), handed out through the
+// same 8 per-XCD heads, bounded by the frames posted so far; so the lanes that frame k's last paths leave idle take
+// frame k+1's items at once.  Which wave traces an item changes nothing: every item runs with the inputs the
+// reference's dispatch of frame k gives its pixel (FrameCount = first_frame + k) and writes its own colour slot.
+//   posting   the host raises the post word (pinned host memory: frames posted | stop << 32).  A wave that finds no
+//             posted unit reads the device mirror of that word; at most one wave per HG_SV_POLL_TICKS reads the host
+//             word itself (a ticket) and raises the mirror by atomic max.
+//   frames    a wave counts, per frame in a window of 4 (LDS), the units it pulled and the items of them its lanes
+//             finished; once they match, after a store drain, it adds the units to the frame's ring-slot count
+//             (frames_done).  Colours go to the frame's ring slot with write-through (sc1) stores: the gate kernel on
+//             the context stream waits for the count (sc1 loads), and the blend after it reads them with sc1 loads
+//             (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + drain + agent atomic / sc1 loads).
+//   leaving   a wave with no item and no posted unit left waits (s_sleep); it leaves once the stop flag is set and
+//             nothing posted is left to claim, or after sv_idle_ticks with nothing posted (the host restarts a server
+//             that has been idle for less than half of that instead of posting to it).
+// Only the lane 0 of a wave runs these (the whole wave converged at the loop top).
+// Per-wave LDS state (lane 0 reads and writes it; the constants are copied from the kernel arguments once, so that no
+// server value stays in a scalar register across the kernel's loop: its scalar registers are all taken, and every
+// value kept live there spilled the traversal's vector registers to scratch — 84 B per lane in the first form)
+struct SvWave {
+    uint32_t view;   // units posted as this wave last saw them
+    uint32_t dry;    // the view at which this wave last found every head dry (HG_NONE: none)
+    uint32_t pend;   // a unit claimed beyond the view, or whose frame window was busy (HG_NONE: none)
+    uint32_t stop;   // the stop flag as this wave last saw it
+    uint32_t nlt, mask, cap, magic, shift, idle_ticks;  // tiles per frame, ring slots - 1, frames cap, u / nlt, leave after
+    uint32_t post_lo, post_hi, done_lo, done_hi;        // the host post word and the ring-slot counts (pointers)
+    uint32_t win_frame[4], win_units[4], win_items[4], win_done[4];  // frame window (k & 3)
+};
+__shared__ SvWave hg_sv;
+
+__device__ __forceinline__ unsigned long long* sv_word64(const HgKernelParams& kp, uint32_t word) {
+    return reinterpret_cast<unsigned long long*>(kp.queue + word);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Device-coherent single words (relaxed agent-scope atomics: written through to / read from the coherent level).  No
-// acquire / release fences: at agent scope on gfx950 those write back or invalidate the XCD's whole L2, and one per
-// wave leaving made 1-frame launches 2x slower (the waves lost their cached nodes); mig_drain orders a lane's stores.
-__device__ __forceinline__ void mig_st(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+template <class T>
+__device__ __forceinline__ T* sv_ptr(uint32_t lo, uint32_t hi) {
+    return reinterpret_cast<T*>((uint64_t(hi) << 32) | lo);
 }
-__device__ __forceinline__ void mig_drain() {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-__device__ __forceinline__ unsigned long long* mig_state(const HgKernelParams& kp) {
-    return reinterpret_cast<unsigned long long*>(kp.queue + HG_MIG_STATE_WORD);
-}
-__device__ __forceinline__ uint4* mig_rec(const HgKernelParams& kp, uint32_t i) {
-    return reinterpret_cast<uint4*>(reinterpret_cast<char*>(kp.queue) + HG_MIG_POOL_BYTE) + 8u * i;
-}
-// the pool's counts in one 64-bit word: records reserved (low half) and taken (high half), one load to test it
-__device__ __forceinline__ unsigned long long* mig_pool(const HgKernelParams& kp) {
-    return reinterpret_cast<unsigned long long*>(kp.queue + HG_MIG_POOL_WORD);
-}
-__device__ __forceinline__ bool mig_pool_empty(const HgKernelParams& kp) {
-    const unsigned long long v = __hip_atomic_load(mig_pool(kp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return uint32_t(v >> 32) >= uint32_t(v);
-}
-// lane 0: retire the wave, unless the pool holds records to take or it would leave fewer than gridDim >> HG_MIG_KEEP_SHIFT
-// waves of the launch not gone (at least one)
-__device__ __forceinline__ bool mig_try_retire(const HgKernelParams& kp) {
-    if (!mig_pool_empty(kp)) return false;
-    unsigned long long* const s = mig_state(kp);
-    unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int t = 0; t < 16; ++t) {
-        if (uint32_t(v) + 1u + (gridDim.x >> HG_MIG_KEEP_SHIFT) > gridDim.x || uint32_t(v) + 1u >= gridDim.x) return false;
-        if (__hip_atomic_compare_exchange_strong(s, &v, v + 1ull + (1ull << 32), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return true;
+__device__ void sv_init(const HgKernelParams& kp) {  // lane 0, at the kernel's start
+    lds_put(hg_sv.view, 0u);
+    lds_put(hg_sv.dry, HG_NONE);
+    lds_put(hg_sv.pend, HG_NONE);
+    lds_put(hg_sv.stop, 0u);
+    lds_put(hg_sv.nlt, uint32_t(kp.n_local_tiles));
+    lds_put(hg_sv.mask, kp.sv_ring - 1u);
+    lds_put(hg_sv.cap, kp.sv_frames_cap);
+    lds_put(hg_sv.magic, kp.sv_div_magic);
+    lds_put(hg_sv.shift, kp.sv_div_shift);
+    lds_put(hg_sv.idle_ticks, kp.sv_idle_ticks);
+    lds_put(hg_sv.post_lo, uint32_t(uintptr_t(kp.sv_post)));
+    lds_put(hg_sv.post_hi, uint32_t(uintptr_t(kp.sv_post) >> 32));
+    lds_put(hg_sv.done_lo, uint32_t(uintptr_t(kp.frames_done)));
+    lds_put(hg_sv.done_hi, uint32_t(uintptr_t(kp.frames_done) >> 32));
+    for (uint32_t w = 0; w < 4u; ++w) {
+        lds_put(hg_sv.win_frame[w], 0u);
+        lds_put(hg_sv.win_units[w], 0u);
+        lds_put(hg_sv.win_items[w], 0u);
+        lds_put(hg_sv.win_done[w], 0u);
     }
-    return false;
 }
-// lane 0 of a wave with no path: leave, if the pool is empty and either another wave is not gone or no retired wave
-// is still exporting (a successful exchange of the word read proves no wave retired since)
-__device__ __forceinline__ bool mig_try_leave(const HgKernelParams& kp) {
-    unsigned long long* const s = mig_state(kp);
-    unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int t = 0; t < 16; ++t) {
-        if (uint32_t(v) + 1u >= gridDim.x && (v >> 32) != 0ull) return false;
-        if (!mig_pool_empty(kp)) return false;
-        if (__hip_atomic_compare_exchange_strong(s, &v, v + 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return true;
+// frame of unit u: u / nlt by the host's multiplier (exact for every u < 2^31; a power of two nlt: magic 0, a shift)
+__device__ __forceinline__ uint32_t sv_frame(uint32_t u) {
+    const uint32_t m = lds_get(hg_sv.magic);
+    return (m ? __umulhi(u, m) : u) >> lds_get(hg_sv.shift);
+}
+// the posted units of a post word value
+__device__ __forceinline__ uint32_t sv_units(unsigned long long w) {
+    const uint32_t cap = lds_get(hg_sv.cap);
+    return (uint32_t(w) < cap ? uint32_t(w) : cap) * lds_get(hg_sv.nlt);
+}
+// Refresh the view from the device mirror of the post word
+__device__ uint32_t sv_view(const HgKernelParams& kp) {
+    uint32_t v = lds_get(hg_sv.view);
+    const unsigned long long m = __hip_atomic_load(sv_word64(kp, HG_SV_MIRROR_WORD), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t u = sv_units(m);
+    if (u > v) {
+        v = u;
+        lds_put(hg_sv.view, v);
     }
-    return false;
+    if (m & HG_SV_STOP) lds_put(hg_sv.stop, 1u);
+    return v;
 }
-// lane 0: claim up to `want` pool records (first in `first`)
-__device__ __forceinline__ uint32_t mig_claim(const HgKernelParams& kp, uint32_t want, uint32_t& first) {
-    unsigned long long* const pool = mig_pool(kp);
-    unsigned long long v = __hip_atomic_load(pool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int t = 0; t < 16; ++t) {
-        const uint32_t p = uint32_t(v), q = uint32_t(v >> 32);
-        if (q >= p) return 0u;
-        const uint32_t n = min(want, p - q);
-        if (__hip_atomic_compare_exchange_strong(pool, &v, v + (uint64_t(n) << 32), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-            first = q;
-            return n;
+// (idle waves) take the host-poll ticket if it is free, read the host word over PCIe (system scope) and raise the
+// mirror; then refresh the view
+__device__ uint32_t sv_poll(const HgKernelParams& kp) {
+    unsigned long long* const ticket = sv_word64(kp, HG_SV_TICKET_WORD);
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (now >= t && __hip_atomic_compare_exchange_strong(ticket, &t, now + HG_SV_POLL_TICKS, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        const unsigned long long h = __hip_atomic_load(
+            sv_ptr<const unsigned long long>(lds_get(hg_sv.post_lo), lds_get(hg_sv.post_hi)), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_max(sv_word64(kp, HG_SV_MIRROR_WORD), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return sv_view(kp);
+}
+// Pull the next posted unit into hg_qu[slot], its items numbered from `base` (empty when there is none for now)
+__device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) {
+    QueueUnit& q = hg_qu[slot];
+    lds_put(q.base, base);
+    lds_put(q.end, base);
+    uint32_t u = lds_get(hg_sv.pend);
+    uint32_t view = lds_get(hg_sv.view);
+    if (u == HG_NONE) {
+        if (view == lds_get(hg_sv.dry)) {  // every head was dry at this view: anything new posted?
+            view = sv_view(kp);
+            if (view == lds_get(hg_sv.dry)) return;
+        }
+        const uint32_t x = blockIdx.x & 7u;
+        for (uint32_t t = 0; t < 8u && u == HG_NONE; ++t) {  // own XCD's head first, then steal
+            const uint32_t h = (x + t) & 7u;
+            if (h + 8u * ld_agent(kp.queue + 32u * h) >= view) continue;
+            u = h + 8u * atomicAdd(kp.queue + 32u * h, 1u);
+        }
+        if (u == HG_NONE) {
+            lds_put(hg_sv.dry, view);
+            return;
         }
     }
-    return 0u;
+    if (u >= view) view = sv_view(kp);
+    const uint32_t k = sv_frame(u), w = k & 3u;
+    if (u >= view || (lds_get(hg_sv.win_units[w]) != 0u && lds_get(hg_sv.win_frame[w]) != k)) {
+        lds_put(hg_sv.pend, u);  // (claimed past the posted frames by a race, or its frame window still busy): later
+        return;
+    }
+    lds_put(hg_sv.pend, HG_NONE);
+    const int tile = ordered_tile(kp, u - k * lds_get(hg_sv.nlt));
+    const uint32_t g = uint32_t(kp.rank) + uint32_t(tile) * uint32_t(kp.n_ranks);
+    const uint32_t ty = g / uint32_t(kp.tiles_x);
+    const uint32_t tx0 = (g - ty * uint32_t(kp.tiles_x)) * HG_TILE, ty0 = ty * HG_TILE;
+    const uint32_t tw = min(uint32_t(HG_TILE), kp.Wu - min(kp.Wu, tx0));
+    const uint32_t th = min(uint32_t(HG_TILE), kp.Hu - min(kp.Hu, ty0));
+    const uint64_t now = wave_clock();
+    unsigned long long* const prev = hg_wave_cost[threadIdx.x >> 6];
+    if (prev) cost_add(prev, now - hg_wave_t0[threadIdx.x >> 6]);
+    hg_wave_cost[threadIdx.x >> 6] = kp.tile_cost ? kp.tile_cost + tile : nullptr;
+    hg_wave_t0[threadIdx.x >> 6] = now;
+    lds_put(q.tile, uint32_t(tile));
+    lds_put(q.tx0, tx0);
+    lds_put(q.ty0, ty0);
+    lds_put(q.tw, tw);
+    lds_put(q.nv, tw * th);
+    lds_put(q.f_begin, k);
+    lds_put(q.nf, 1u);
+    lds_put(q.end, base + tw * th);
+    lds_put(hg_sv.win_frame[w], k);
+    lds_put(hg_sv.win_units[w], lds_get(hg_sv.win_units[w]) + 1u);
+    lds_put(hg_sv.win_items[w], lds_get(hg_sv.win_items[w]) + tw * th);
 }
-#endif
-
-#ifndef HG_RAY_SORT
-#define HG_RAY_SORT 0  // A/B (DESIGN.md §10 lever 7): 1 = sort the lanes beginning a ray by direction octant, 2 = by
-                       // octant and dominant axis (24 keys), before their traversal
-#endif
-#if HG_RAY_SORT
-// Ray-coherence experiment.  A vector load costs the texture-data unit per distinct cache line in each 16-lane quarter
-// of the wave, not per line of the whole wave (tools/micro_lane_order.hip: 4 lines per instruction cost 19 cycles with
-// each line's lanes in one quarter and 51-65 with them spread), so rays that visit the same nodes should sit in the same
-// quarter.  The lanes that begin a ray in a shading pass (`began`) exchange their whole path state so that equal sort
-// keys are adjacent: a counting sort of the keys by ballots; lane l writes its own lane number to LDS word pos(l) of the
-// scratch row; the began lane of rank r among the began lanes reads word r, the lane whose state it takes; every state
-// word moves by ds_bpermute (full EXEC: the other lanes take their own).  Which lane runs a path changes no result.
-__device__ __forceinline__ uint32_t ray_key(const f3& d) {
-    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-#if HG_RAY_SORT == 2
-    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-    const uint32_t dom = ax >= ay && ax >= az ? 0u : ay >= az ? 1u : 2u;
-    return oct * 3u + dom;
-#else
-    return oct;
-#endif
+// Frames of the window whose pulled items the lanes have all finished: after a drain of the wave's colour stores, their
+// units go to the frame's ring-slot count
+__device__ void sv_flush() {
+    bool drained = false;
+    for (uint32_t w = 0; w < 4u; ++w) {
+        const uint32_t n = lds_get(hg_sv.win_units[w]);
+        if (n == 0u || lds_get(hg_sv.win_done[w]) != lds_get(hg_sv.win_items[w])) continue;
+        if (!drained) {  // every lane's write-through colour stores complete before the count moves
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            drained = true;
+        }
+        uint32_t* const done = sv_ptr<uint32_t>(lds_get(hg_sv.done_lo), lds_get(hg_sv.done_hi));
+        __hip_atomic_fetch_add(done + 32u * (lds_get(hg_sv.win_frame[w]) & lds_get(hg_sv.mask)), n, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        lds_put(hg_sv.win_units[w], 0u);
+        lds_put(hg_sv.win_items[w], 0u);
+        lds_put(hg_sv.win_done[w], 0u);
+    }
 }
-constexpr uint32_t kRayKeys = HG_RAY_SORT == 2 ? 24u : 8u;
-__device__ __forceinline__ uint32_t bperm(uint32_t src, uint32_t v) {
-    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
+// Loop top: flush finished frames, keep both units filled (the spent one refilled after the other; both spent: two
+// new units, in turn).  Returns true when the wave has no item to hand out now.
+__device__ bool sv_refill(const HgKernelParams& kp) {
+    sv_flush();
+    const uint32_t cnt = lds_get(hg_next_item);
+    uint32_t a = lds_get(hg_q_cur);
+    if (cnt >= lds_get(hg_qu[a].end)) {  // the first unit is spent
+        const uint32_t b_end = lds_get(hg_qu[a ^ 1u].end);
+        const bool both = cnt >= b_end;
+        if (!both) lds_put(hg_q_cur, a ^ 1u);  // the second one is in use: it comes first now
+        for (uint32_t i = 0; i < (both ? 2u : 1u); ++i) {  // (one inlined pull: every copy costs the loop registers)
+            const uint32_t slot = a ^ i;
+            sv_pull(kp, slot, i ? lds_get(hg_qu[a].end) : both ? cnt : b_end);
+        }
+        if (!both) a ^= 1u;
+    }
+    return cnt >= lds_get(hg_qu[a ^ 1u].end) && cnt >= lds_get(hg_qu[a].end);
 }
-__device__ __forceinline__ float bpermf(uint32_t src, float v) { return __uint_as_float(bperm(src, __float_as_uint(v))); }
-#endif
+// A wave with no path: poll (the host word through the ticket) and wait until a unit is posted (returns 0: refill) or
+// it may leave (1)
+__device__ uint32_t sv_wait(const HgKernelParams& kp) {
+    hg_wave_cost[threadIdx.x >> 6] = nullptr;  // the wait is no tile's cost
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 0;; ++spin) {
+        const uint32_t view = sv_poll(kp);
+        const uint32_t pend = lds_get(hg_sv.pend);
+        bool open = pend != HG_NONE && pend < view;
+        for (uint32_t h = 0; h < 8u && !open; ++h) open = h + 8u * ld_agent(kp.queue + 32u * h) < view;
+        if (open) {
+            lds_put(hg_sv.dry, HG_NONE);
+            return 0u;
+        }
+        if (lds_get(hg_sv.stop)) return 1u;  // the final post word: nothing posted is left to claim
+        if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(lds_get(hg_sv.idle_ticks))) return 1u;
+        if (spin < 64u) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(16);
+    }
+}
+// Write-through colour store of a server frame (8-B sc1 stores: device-coherent at the memory side)
+__device__ __forceinline__ void fc_store_wt(float4* p, float4 v) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, (static_cast<unsigned long long>(__float_as_uint(v.y)) << 32) | __float_as_uint(v.x),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (static_cast<unsigned long long>(__float_as_uint(v.w)) << 32) | __float_as_uint(v.z),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Streaming variant (HG_KERNEL_MEGA_STREAM): the regenerating kernel with a resumable traversal.  Lanes advance
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
@@ -1072,8 +1121,10 @@ __device__ __forceinline__ float bpermf(uint32_t src, float v) { return __uint_a
 // their traversal state, so the wave's lanes stay busy instead of waiting for the slowest ray of every bounce.
 // Every frame's colour goes to frame_color (item scheduling), blended in frame order by hg_blend_frames.  kQueue: the
 // persistent work-queue form above (launches of few frames).
-template <bool kCounters, bool kMeshLds, bool kQueue, bool kDeep>
+// kServer (with kQueue): the render server's persistent form above.
+template <bool kCounters, bool kMeshLds, bool kQueue, bool kDeep, bool kServer>
 __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream_kernel(const HgKernelParams kp) {
+    static_assert(!kServer || kQueue, "the render server is a queue launch");
     // shade once at most kTmin lanes still traverse; reshade while at least kReshade need it (compile-time: as kernel
     // parameters they cost 8 B of scratch)
     constexpr uint32_t kTmin = kDeep ? HG_STREAM_TMIN_DEEP : HG_STREAM_TMIN;
@@ -1093,11 +1144,12 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             lds_put(hg_q_cur, 0u);
             lds_put(hg_q_dry, 0u);
             hg_wave_cost[threadIdx.x >> 6] = nullptr;
+            if constexpr (kServer) sv_init(kp);
         }
     } else {
         // wave -> (tile, frame chunk), as in hg_trace_regen_kernel
         // one wave per workgroup (launched with 64 threads): wave = workgroup
-        const uint32_t gw = xcd_block(blockIdx.x, gridDim.x);
+        const uint32_t gw = blockIdx.x;
         u_first = gw * (kp.wave_units > 1u ? kp.wave_units : 1u);  // (more than one unit only without a frame split)
         wave_unit(kp, u_first, nlt, split, local_tile, chunk);
         tile_cost_begin(kp, lane, local_tile, chunk < split);
@@ -1114,18 +1166,6 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         mesh_lds_fill(kp, lane);
         wave_lds_sync();
     }
-#if HG_NODE_CACHE
-    {  // the wave's copy of the hot node records (written before any lane reads it: one wave per workgroup)
-        float4* cache = reinterpret_cast<float4*>(hg_lds_stack + kRowCache * 64u);
-        const uint32_t nf4 = 4u * (kp.hot_records < HG_NODE_CACHE ? kp.hot_records : uint32_t(HG_NODE_CACHE));
-        for (uint32_t i = lane; i < nf4; i += 64u) cache[i] = kp.nodes[i];
-        wave_lds_sync();
-    }
-#endif
-#if HG_WAVE_TIMELINE
-    uint64_t tl_start = 0, tl_dry = 0;
-    if (kQueue && kp.timeline) tl_start = __builtin_amdgcn_s_memrealtime();
-#endif
     bool work = false;
     uint32_t px = 0u, py = 0u;
     Counters c{0, 0, 0, 0, 0, 0, 0, 0};
@@ -1140,12 +1180,6 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     tv.mi = nm;
     uint32_t slot = 0;  // the lane's item: kQueue its accumulator slot (local tile * 64 + pixel), else v (UnitItems)
     bool dry = false;   // kQueue, wave-uniform: the queue has no unit left
-#if HG_MIG_KERNEL
-    // (kQueue, wave-uniform) 1: the wave exports its paths at their ray boundaries, then leaves.  The kernel is at
-    // its scalar-register limit: every wave-uniform value live across the loop spills (a lane holding an imported
-    // path is marked by its mesh cursor, tv.mi = nm + 1, not by a mask)
-    uint32_t retiring = 0;
-#endif
     const UnitItems items = kQueue ? UnitItems() : UnitItems(kp, u_first, local_tile, chunk < split, f_begin, f_end, lane);
     if constexpr (kQueue) {
         wave_lds_sync();  // hg_q / hg_next_item initialised (lane 0); every lane takes its first item in the loop
@@ -1168,355 +1202,194 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
         }
     }
     uint64_t cyc_trav = 0, cyc_shade = 0;  // wave clock (s_memtime) per phase, counting instantiation only
-#if HG_DRAIN_PRIO
-    __builtin_amdgcn_s_setprio(2);
-#elif HG_SHADE_PRIO >= 2
-    __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);  // traversal waits on memory: its waves issue first
-#endif
-    for (;;) {
-        // ---- kQueue: the wave refills a spent unit, and idle lanes (the wave's start; lanes whose take found both
-        // units spent) become fresh: they take their item in the shading pass below
-        if (kQueue && !dry) {
-            wave_lds_sync();
-            if (lane == 0u) lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
-            wave_lds_sync();
-            dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
-#if HG_WAVE_TIMELINE
-            if (dry && kp.timeline) tl_dry = __builtin_amdgcn_s_memrealtime();
-#endif
-            if (!work && !dry) {
-                work = true;
-                bounce = kFreshLane;
-                tv.mi = nm;
-            }
+    __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);  // traversal waits on memory: its waves issue first
+    for (;;) {  // (kServer: once per stretch of posted work; the others: once)
+        if constexpr (kServer) {  // (no path in flight: the state starts afresh, so none of it is live across the wait)
+            work = false;
+            ray = Ray{mk(0, 0, 0), mk(0, 0, 1)};
+            tv = Trav{};
+            tv.mi = nm;
+            smp = Sampler{0u, 0u, 0u};
+            ms = MediumStack{0ull, 0};
+            fs = bounce = slot = 0u;
+            acc_rough = 0.0f;
         }
-#if HG_MIG_KERNEL
-        if (kQueue && dry) {  // (the whole wave converged)
-            if (retiring) {
-                if (!__any(work)) {  // every path exported or finished
-                    mig_drain();  // (the wave's records are flagged before it stops counting as exporting)
-                    if (lane == 0u)
-                        __hip_atomic_fetch_add(mig_state(kp), 0xFFFFFFFF00000000ull, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            } else {
-                // idle lanes take exported paths (their state as the exporting lane left it at a ray boundary)
-                // (each test of the pool is a device-coherent load, microseconds: a wave with most lanes busy tests it
-                // every HG_MIG_POLL-th loop only)
-                bool leave_now = false, poll = false;
-                uint32_t mig_spins = 0;
-                for (;;) {  // (an inner loop: a second latch of the outer loop cost the kernel scratch)
-                const uint64_t idle = wave_ballot(!work);
-                const uint32_t n_idle = uint32_t(__builtin_popcountll(idle));
-                poll = n_idle >= uint32_t(HG_MIG_POLL_IDLE);
-                uint32_t n = 0, q0 = 0;
-                if (poll && lane == 0u) n = mig_claim(kp, n_idle, q0);
-                n = __builtin_amdgcn_readfirstlane(n);
-                q0 = __builtin_amdgcn_readfirstlane(q0);
-                const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
-                if (!work && r < n) {
-                    uint4* const rec = mig_rec(kp, q0 + r);
-                    uint32_t* const flag = &rec[6].x;
-                    uint32_t s1 = mig_ld(flag);
-                    for (uint32_t k = 0; s1 == 0u && k < (1u << 22); ++k) {  // (reserved: its writer is resident)
-                        __builtin_amdgcn_s_sleep(1);
-                        s1 = mig_ld(flag);
-                    }
-                    const uint32_t* const w = reinterpret_cast<const uint32_t*>(rec);
-                    ray.o = mk(__uint_as_float(mig_ld(w + 0)), __uint_as_float(mig_ld(w + 1)), __uint_as_float(mig_ld(w + 2)));
-                    ray.d = mk(__uint_as_float(mig_ld(w + 3)), __uint_as_float(mig_ld(w + 4)), __uint_as_float(mig_ld(w + 5)));
-                    s_thr.set(mk(__uint_as_float(mig_ld(w + 6)), __uint_as_float(mig_ld(w + 7)), __uint_as_float(mig_ld(w + 8))));
-                    s_col.set(mk(__uint_as_float(mig_ld(w + 9)), __uint_as_float(mig_ld(w + 10)), __uint_as_float(mig_ld(w + 11))));
-                    acc_rough = __uint_as_float(mig_ld(w + 12));
-                    fs = mig_ld(w + 13);
-                    bounce = mig_ld(w + 14);
-                    smp.frame = mig_ld(w + 15);
-                    smp.pixel = mig_ld(w + 16);
-                    smp.offset = mig_ld(w + 17);
-                    ms.s = uint64_t(mig_ld(w + 18)) | (uint64_t(mig_ld(w + 19)) << 32);
-                    ms.sp = int(mig_ld(w + 20));
-                    __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    slot = s1 - 1u;
-                    work = true;
-                    tv.mi = nm + 1u;  // waits to shade: the shading pass begins its ray
-                }
-                if (__any(work)) break;
-                uint32_t leave = 0;
-                if (lane == 0u) leave = mig_try_leave(kp) ? 1u : 0u;
-                if (__builtin_amdgcn_readfirstlane(leave) || ++mig_spins >= (1u << 22)) {
-                    leave_now = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);  // the launch's last wave: exporters are still at work
-                }
-                if (leave_now) break;
-                if (poll && kp.spp == 1 && wave_count(work) <= uint32_t(HG_MIG_RETIRE)) {  // (a sample sum stays)
-                    uint32_t ret = 0;
-                    if (lane == 0u) ret = mig_try_retire(kp) ? 1u : 0u;
-                    retiring = __builtin_amdgcn_readfirstlane(ret);
-                }
-            }
-        }
-#endif
-        if (!__any(work)) break;
-        // ---- traversal rounds until few lanes are left traversing
-        if (kCounters) cyc_trav -= wave_clock();
         for (;;) {
-            const bool act = work && tv.mi < nm;
-            const uint64_t am = wave_ballot(act);
-            // (work includes act: some lane waits to shade iff the work mask differs)
-            if (am == 0ull || (uint32_t(__builtin_popcountll(am)) <= kTmin && wave_ballot(work) != am)) break;
-            trav_step<kMeshLds>(kp, ray, tv, c, stk, act, ls);
-        }
-        if (kCounters) {
-            const uint64_t t = wave_clock();
-            cyc_trav += t;
-            cyc_shade -= t;
-        }
-#if HG_DRAIN_PRIO  // (A/B) a queue wave past its queue's end drains at the lowest priority in both phases
-        if (kQueue && dry) __builtin_amdgcn_s_setprio(0);
-        else __builtin_amdgcn_s_setprio(1);
-#elif HG_SHADE_PRIO == 1
-        __builtin_amdgcn_s_setprio(1);
-#elif HG_SHADE_PRIO >= 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
-        // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
-        // (rays that finish at once — everything culled — shade again in this loop while at least
-        // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
-        for (uint32_t it = 0;; ++it) {
-            const uint32_t n_sh = wave_count(work && tv.mi >= nm);
-            if (n_sh == 0u || (it > 0u && n_sh < kReshade)) break;
-#if HG_RAY_SORT
-            bool began = false;  // this lane begins a ray (its traversal starts after the sort below)
-#endif
-            if (work && tv.mi >= nm) {
-            c.shade_rounds += wave_once();
-#if HG_PHASE_DETAIL == 1
-            uint64_t tp = kCounters ? wave_clock() : 0;
-#endif
-            const bool fresh = kQueue && bounce == kFreshLane;  // no path yet: straight to the take below
-#if HG_MIG_KERNEL
-            const bool imported = kQueue && tv.mi == nm + 1u;  // begin the imported path's ray
-#else
-            constexpr bool imported = false;
-#endif
-            bool alive = imported;
-            f3 thr = s_thr.get(), col = s_col.get();
-            if (!fresh && !imported) {
-            const Hit hit = trav_hit<kMeshLds>(kp, ray, tv);
-#if HG_PHASE_DETAIL == 1
-            if (kCounters) tp = phase_mark(kp, 11, tp);
-#endif
-            if (hit.t < kp.far_) {  // :898-936
-                c.hits++;
-                const Mat mt = load_mat(kp, hit.mat);
-                col = col + xyz(mt.emis_rough) * thr;
-                uint32_t bt = 0;
-                const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);
-                bounce += 1u << (8u * bt);
-                thr = thr * att;
-                acc_rough += mt.emis_rough.w * thr.x;
-                const float rr = smp.get1(ID_RR);
-                smp.offset += BOUNCE_INC;
-                const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
-                if (!(rr > contribution)) {
-                    thr = thr * rcp_exact(contribution);
-                    bounce += 1u << 24;
-                    alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
-                                                                 ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
-                                                                 ((bounce >> 16) & 0xFFu) > kp.max_trans);
+            // ---- kQueue: the wave refills a spent unit, and idle lanes (the wave's start; lanes whose take found both
+            // units spent) become fresh: they take their item in the shading pass below
+            if constexpr (kServer) {
+                wave_lds_sync();
+                if (lane == 0u) lds_put(hg_q_empty, sv_refill(kp) ? 1u : 0u);
+                wave_lds_sync();
+                if (!work && __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) == 0u) {
+                    work = true;
+                    bounce = kFreshLane;
+                    tv.mi = nm;
                 }
-            } else {  // :941
-                c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
-                col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
+            } else if (kQueue && !dry) {
+                wave_lds_sync();
+                if (lane == 0u) lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
+                wave_lds_sync();
+                dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
+                if (!work && !dry) {
+                    work = true;
+                    bounce = kFreshLane;
+                    tv.mi = nm;
+                }
             }
+            if (!__any(work)) break;
+            // ---- traversal rounds until few lanes are left traversing
+            if (kCounters) cyc_trav -= wave_clock();
+            for (;;) {
+                const bool act = work && tv.mi < nm;
+                const uint64_t am = wave_ballot(act);
+                // (work includes act: some lane waits to shade iff the work mask differs)
+                if (am == 0ull || (uint32_t(__builtin_popcountll(am)) <= kTmin && wave_ballot(work) != am)) break;
+                trav_step<kMeshLds>(kp, ray, tv, c, stk, act, ls);
             }
-#if HG_PHASE_DETAIL == 1
-            if (kCounters) tp = phase_mark(kp, 12, tp);
-#endif
-            if (!alive) {
-                // RayColor += trace_ray(...); spp 1: the sum is the path's colour (0 + col == col bit for bit: col
-                // is never -0, it starts at +0 and only has terms added)
-                const bool one_sample = kp.spp == 1;
-                f3 sum = one_sample ? col : s_sum.get() + col;
-                ++fs;
-                bool next = !fresh && (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
-                if (!next) {
-                    const f3 color = sample_mean(kp, sum);
-                    const size_t slot_i = kQueue ? size_t(slot) : size_t(items.slot(slot));
-                    // this frame's colour, blended later in frame order (hg_blend_frames)
-#if !HG_DIAG_NO_FC  // (analysis builds only: the write-traffic attribution of DESIGN.md §4.5)
-                    if (!fresh)
-                        fc_store(kp.frame_color + fc_index(kp, fs >> 16, slot_i), make_float4(color.x, color.y, color.z, 1.0f));
-#endif
-                    fs = (fs & 0xFFFF0000u) + 0x10000u;
-                    if constexpr (kQueue) {
-                        uint32_t f = 0, hx = 0, hy = 0;
-                        if (queue_item(queue_take(), slot, f, hx, hy)) {  // the unit's next item: statics reset
-                            next = true;
-                            sum = mk(0, 0, 0);
-                            fs = f << 16;
-                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
-                                          0u};
-                            ms = MediumStack{0ull, 0};
+            if (kCounters) {
+                const uint64_t t = wave_clock();
+                cyc_trav += t;
+                cyc_shade -= t;
+            }
+            __builtin_amdgcn_s_setprio(0);
+            // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
+            // (rays that finish at once — everything culled — shade again in this loop while at least
+            // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
+            for (uint32_t it = 0;; ++it) {
+                const uint32_t n_sh = wave_count(work && tv.mi >= nm);
+                if (n_sh == 0u || (it > 0u && n_sh < kReshade)) break;
+                if (work && tv.mi >= nm) {
+                c.shade_rounds += wave_once();
+                const bool fresh = kQueue && bounce == kFreshLane;  // no path yet: straight to the take below
+                bool alive = false;
+                f3 thr = s_thr.get(), col = s_col.get();
+                if (!fresh) {
+                const Hit hit = trav_hit<kMeshLds>(kp, ray, tv);
+                if (hit.t < kp.far_) {  // :898-936
+                    c.hits++;
+                    const Mat mt = load_mat(kp, hit.mat);
+                    col = col + xyz(mt.emis_rough) * thr;
+                    uint32_t bt = 0;
+                    const f3 att = evaluate_hit(kp, smp, ms, ray, hit, mt, bt);
+                    bounce += 1u << (8u * bt);
+                    thr = thr * att;
+                    acc_rough += mt.emis_rough.w * thr.x;
+                    const float rr = smp.get1(ID_RR);
+                    smp.offset += BOUNCE_INC;
+                    const float contribution = fmaxf(fmaxf(thr.x, thr.y), thr.z);
+                    if (!(rr > contribution)) {
+                        thr = thr * rcp_exact(contribution);
+                        bounce += 1u << 24;
+                        alive = (bounce >> 24) <= kp.max_bounces && !((bounce & 0xFFu) > kp.max_diff ||
+                                                                     ((bounce >> 8) & 0xFFu) > kp.max_glossy ||
+                                                                     ((bounce >> 16) & 0xFFu) > kp.max_trans);
+                    }
+                } else {  // :941
+                    c.primary_miss += bounce == 0u;  // the path's camera ray (no bounce recorded yet)
+                    col = col + sample_sky(kp, ray.d, sky_level(kp, acc_rough)) * thr;
+                }
+                }
+                if (!alive) {
+                    // RayColor += trace_ray(...); spp 1: the sum is the path's colour (0 + col == col bit for bit: col
+                    // is never -0, it starts at +0 and only has terms added)
+                    const bool one_sample = kp.spp == 1;
+                    f3 sum = one_sample ? col : s_sum.get() + col;
+                    ++fs;
+                    bool next = !fresh && (fs & 0xFFFFu) < kp.spp;  // next sample: statics persist (:188-189)
+                    if (!next) {
+                        const f3 color = sample_mean(kp, sum);
+                        const size_t slot_i = kQueue ? size_t(slot) : size_t(items.slot(slot));
+                        // this frame's colour, blended later in frame order (hg_blend_frames*; the server's gate + blend)
+                        if constexpr (kServer) {
+                            if (!fresh) {
+                                const uint32_t k = smp.frame - uint32_t(kp.first_frame);  // the server's frame index
+                                fc_store_wt(kp.frame_color + size_t(k & lds_get(hg_sv.mask)) * (lds_get(hg_sv.nlt) * 64u) + slot_i,
+                                            make_float4(color.x, color.y, color.z, 1.0f));
+                                atomicAdd(&hg_sv.win_done[k & 3u], 1u);  // (LDS) one more item of frame k finished
+                            }
+                        } else if (!fresh) {
+                            fc_store(kp.frame_color + fc_index(kp, fs >> 16, slot_i), make_float4(color.x, color.y, color.z, 1.0f));
                         }
+                        fs = (fs & 0xFFFF0000u) + 0x10000u;
+                        if constexpr (kQueue) {
+                            uint32_t f = 0, hx = 0, hy = 0;
+                            if (queue_item(queue_take(), slot, f, hx, hy)) {  // the unit's next item: statics reset
+                                next = true;
+                                sum = mk(0, 0, 0);
+                                fs = kServer ? 0u : f << 16;  // (the server's frame index is smp.frame - first_frame)
+                                smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
+                                              0u};
+                                ms = MediumStack{0ull, 0};
+                            }
+                        } else {
+                            const uint32_t k = items.take_here();
+                            if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
+                                uint32_t f, hx, hy;
+                                items.get(kp, k, slot, f);
+                                items.pixel(slot, hx, hy);
+                                next = true;
+                                sum = mk(0, 0, 0);
+                                fs = f << 16;
+                                smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
+                                              0u};
+                                ms = MediumStack{0ull, 0};
+                            }
+                        }
+                    }
+                    if (!one_sample) s_sum.set(sum);
+                    if (next) {
+                        {
+                            uint32_t qx, qy;
+                            if constexpr (kQueue) slot_pixel(kp, slot, qx, qy);
+                            else items.pixel(slot, qx, qy);
+                            ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
+                        }
+                        thr = mk(1, 1, 1);
+                        col = mk(0, 0, 0);
+                        acc_rough = 0.0f;
+                        bounce = 0;
+                        paths++;
+                        alive = true;
                     } else {
-                        const uint32_t k = items.take_here();
-                        if (k < items.n_items) {  // the next (pixel, frame) item: statics reset as for a dispatch
-                            uint32_t f, hx, hy;
-                            items.get(kp, k, slot, f);
-                            items.pixel(slot, hx, hy);
-                            next = true;
-                            sum = mk(0, 0, 0);
-                            fs = f << 16;
-                            smp = Sampler{kp.accumulate ? uint32_t(kp.first_frame) + f : 1u, pcg_hash(hx + hy * kp.Wu),
-                                          0u};
-                            ms = MediumStack{0ull, 0};
-                        }
+                        work = false;
                     }
                 }
-                if (!one_sample) s_sum.set(sum);
-                if (next) {
-                    {
-                        uint32_t qx, qy;
-                        if constexpr (kQueue) slot_pixel(kp, slot, qx, qy);
-                        else items.pixel(slot, qx, qy);
-                        ray = camera_ray(kp, smp, (float(qx) / kp.W) * 2.0f - 1.0f, (float(qy) / kp.H) * 2.0f - 1.0f);
-                    }
-                    thr = mk(1, 1, 1);
-                    col = mk(0, 0, 0);
-                    acc_rough = 0.0f;
-                    bounce = 0;
-                    paths++;
-                    alive = true;
-                } else {
-                    work = false;
+                s_thr.set(thr);
+                s_col.set(col);
+                if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
                 }
             }
-            s_thr.set(thr);
-            s_col.set(col);
-#if HG_PHASE_DETAIL == 1
-            if (kCounters) tp = phase_mark(kp, 13, tp);
-#endif
-#if HG_MIG_KERNEL
-            if (kQueue && retiring && alive) {  // export the path at its ray boundary (taken by a staying wave)
-                const uint64_t m = __builtin_amdgcn_read_exec();
-                const uint32_t rk = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                uint32_t b0 = 0;
-                if (rk == 0u) b0 = uint32_t(atomicAdd(mig_pool(kp), (unsigned long long)__builtin_popcountll(m)));
-                uint4* const rec = mig_rec(kp, __builtin_amdgcn_readfirstlane(b0) + rk);
-                uint32_t* const w = reinterpret_cast<uint32_t*>(rec);
-                const uint32_t v[21] = {__float_as_uint(ray.o.x), __float_as_uint(ray.o.y), __float_as_uint(ray.o.z),
-                                        __float_as_uint(ray.d.x), __float_as_uint(ray.d.y), __float_as_uint(ray.d.z),
-                                        __float_as_uint(thr.x), __float_as_uint(thr.y), __float_as_uint(thr.z),
-                                        __float_as_uint(col.x), __float_as_uint(col.y), __float_as_uint(col.z),
-                                        __float_as_uint(acc_rough), fs, bounce, smp.frame, smp.pixel, smp.offset,
-                                        uint32_t(ms.s), uint32_t(ms.s >> 32), uint32_t(ms.sp)};
-#pragma unroll
-                for (int k = 0; k < 21; ++k) mig_st(w + k, v[k]);
-                mig_drain();  // the record's words are out before its flag
-                mig_st(w + 24, slot + 1u);
-                alive = false;
-                work = false;
-            }
-#endif
-#if HG_RAY_SORT
-            began = alive;
-#else
-            if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
-#endif
-#if HG_PHASE_DETAIL == 1
-            if (kCounters) tp = phase_mark(kp, 14, tp);
-#endif
-            }
-#if HG_RAY_SORT
-            {  // converged: permute the began lanes' path states into key order, then begin their traversals
-                const uint64_t bm = wave_ballot(began);
-                if (__builtin_popcountll(bm) >= 2) {
-                    const uint32_t key = began ? ray_key(ray.d) : kRayKeys;
-                    uint32_t pos = 0, base = 0;
-                    for (uint32_t v = 0; v < kRayKeys; ++v) {
-                        const uint64_t m = wave_ballot(key == v);
-                        if (key == v)
-                            pos = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                        base += uint32_t(__builtin_popcountll(m));
-                    }
-                    uint32_t* const scratch = hg_lds_stack + kRowSort * 64u;
-                    if (began) scratch[pos] = lane;
-                    wave_lds_sync();
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
-                    const uint32_t src = began ? scratch[rank] : lane;
-                    wave_lds_sync();
-                    ray.o = mk(bpermf(src, ray.o.x), bpermf(src, ray.o.y), bpermf(src, ray.o.z));
-                    ray.d = mk(bpermf(src, ray.d.x), bpermf(src, ray.d.y), bpermf(src, ray.d.z));
-                    fs = bperm(src, fs);
-                    bounce = bperm(src, bounce);
-                    smp.frame = bperm(src, smp.frame);
-                    smp.pixel = bperm(src, smp.pixel);
-                    smp.offset = bperm(src, smp.offset);
-                    ms.s = (uint64_t(bperm(src, uint32_t(ms.s >> 32))) << 32) | bperm(src, uint32_t(ms.s));
-                    ms.sp = int(bperm(src, uint32_t(ms.sp)));
-                    acc_rough = bpermf(src, acc_rough);
-                    slot = bperm(src, slot);
-                    const RowVec3<kRowThr> o_thr{src};
-                    const RowVec3<kRowCol> o_col{src};
-                    const f3 t_thr = o_thr.get(), t_col = o_col.get();
-                    f3 t_sum = mk(0, 0, 0);
-                    if (kp.spp != 1) t_sum = RowVec3<kRowSum>{src}.get();
-                    wave_lds_sync();
-                    s_thr.set(t_thr);
-                    s_col.set(t_col);
-                    if (kp.spp != 1) s_sum.set(t_sum);
-                    wave_lds_sync();
-                }
-                if (began) trav_begin<kMeshLds>(kp, ray, tv, c);
-            }
-#endif
+            __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
+            if (kCounters) cyc_shade += wave_clock();
         }
-#if HG_DRAIN_PRIO
-        if (kQueue && dry) __builtin_amdgcn_s_setprio(0);
-        else __builtin_amdgcn_s_setprio(2);
-#elif HG_SHADE_PRIO == 1
-        __builtin_amdgcn_s_setprio(0);
-#elif HG_SHADE_PRIO >= 2
-        __builtin_amdgcn_s_setprio(HG_SHADE_PRIO - 1);
-#endif
-        if (kCounters) cyc_shade += wave_clock();
+        if constexpr (!kServer) {
+            break;
+        } else {
+            // no path in flight and no item to hand out: wait for the host's next frame (polling the host word), or
+            // leave.  Outside the tracing loop, where no path state is live (its registers stay the tracing loop's).
+            wave_lds_sync();
+            if (lane == 0u) lds_put(hg_q_empty, sv_wait(kp));
+            wave_lds_sync();
+            if (__builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u) break;
+        }
     }
     if constexpr (kQueue) record_tile_cost(lane);
     else items.record_cost(kp, lane);
-#if HG_WAVE_TIMELINE
-    if (kQueue && kp.timeline && lane == 0u && blockIdx.x < HG_TIMELINE_WAVES) {
-        unsigned long long* const w = kp.timeline + 4u * blockIdx.x;
-        w[0] = tl_start;
-        w[1] = tl_dry;
-        w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = lds_get(hg_next_item);
-    }
-#endif
-    if constexpr (kQueue) {
+    if constexpr (kQueue && !kServer) {
         // The last wave out resets the queue heads for the next launch on this stream (no memset launch per queue
         // launch: a blit kernel waited for a CU that the other streams' persistent waves held).  A wave leaves only
-        // once its pulls found the queue dry, and it pulls no more after that: every head access of the launch
-        // happens before the last wave's increment of the exit count (release / acquire).
+        // once its pulls found the queue dry, and it pulls no more after that: every head atomic of the launch has
+        // returned before the last wave's increment of the exit count.  Relaxed: an agent-scope acquire / release is
+        // a write-back / invalidate of the XCD's whole L2 on gfx950, per wave leaving (strict C3 +1.3 %, a display
+        // one frame behind +3.4 % without it; DESIGN.md section 10 lever 13); the next launch on this stream starts
+        // after this one's end.
         if (lane == 0u) {
-#if HG_QUEUE_DONE_RELAXED  // (A/B) the head atomics all returned before each wave's increment: no L2 write-back /
-                           // invalidate of the XCD per wave leaving
             const uint32_t out = __hip_atomic_fetch_add(kp.queue + HG_QUEUE_DONE_WORD, 1u, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
-#else
-            const uint32_t out = __hip_atomic_fetch_add(kp.queue + HG_QUEUE_DONE_WORD, 1u, __ATOMIC_ACQ_REL,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-#endif
             if (out == gridDim.x - 1u) {
                 for (uint32_t h = 0; h < 8u; ++h)
                     __hip_atomic_store(kp.queue + 32u * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if HG_MIG_KERNEL
-                __hip_atomic_store(mig_state(kp), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(mig_pool(kp), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
                 __hip_atomic_store(kp.queue + HG_QUEUE_DONE_WORD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
@@ -1540,7 +1413,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     }
 }
 
-hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream) {
+hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool counters, hipStream_t stream, bool server) {
     (void)block;  // one wave per workgroup (the kernel's LDS rows assume it)
     int64_t grid = int64_t(kp_in.n_local_tiles) * kp_in.frame_split;
     const bool queue = kp_in.queue != nullptr;  // the runtime passes a queue for launches of few frames
@@ -1549,19 +1422,25 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
         grid = (grid + kp_in.wave_units - 1) / kp_in.wave_units;
     if (grid == 0) return hipSuccess;
     const uint32_t lds_depth = kp_in.stack_depth < HG_STREAM_LDS_STACK ? kp_in.stack_depth : HG_STREAM_LDS_STACK;
-    const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t) + HG_STREAM_LDS_PAD;
+    const size_t lds = size_t(kRowStack + lds_depth) * 64u * sizeof(uint32_t);
     HgKernelParams kp = kp_in;
     kp.mesh_lds_word = uint32_t(lds / 4u);
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
     const dim3 g{uint32_t(grid)}, b{64u};
     const size_t sh = mesh_lds ? mesh_lds : lds;
     // deep BLAS (kp.stream_deep): the kDeep thresholds
-#define HG_STREAM_LAUNCH(C, M, Q)                                                                                      \
+#define HG_STREAM_LAUNCH_S(C, M, Q, S)                                                                                 \
     do {                                                                                                               \
-        if (kp.stream_deep) hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, true>), g, b, sh, stream, kp);        \
-        else hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, false>), g, b, sh, stream, kp);                      \
+        if (kp.stream_deep) hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, true, S>), g, b, sh, stream, kp);     \
+        else hipLaunchKernelGGL((hg_trace_stream_kernel<C, M, Q, false, S>), g, b, sh, stream, kp);                   \
     } while (0)
-    if (queue) {
+#define HG_STREAM_LAUNCH(C, M, Q) HG_STREAM_LAUNCH_S(C, M, Q, false)
+    if (server) {
+        if (counters && mesh_lds) HG_STREAM_LAUNCH_S(true, true, true, true);
+        else if (counters) HG_STREAM_LAUNCH_S(true, false, true, true);
+        else if (mesh_lds) HG_STREAM_LAUNCH_S(false, true, true, true);
+        else HG_STREAM_LAUNCH_S(false, false, true, true);
+    } else if (queue) {
         if (counters && mesh_lds) HG_STREAM_LAUNCH(true, true, true);
         else if (counters) HG_STREAM_LAUNCH(true, false, true);
         else if (mesh_lds) HG_STREAM_LAUNCH(false, true, true);
@@ -1573,6 +1452,51 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
         else HG_STREAM_LAUNCH(false, false, false);
     }
 #undef HG_STREAM_LAUNCH
+#undef HG_STREAM_LAUNCH_S
+    return hipGetLastError();
+}
+
+// The render server's per-frame work on the context stream (hg_runtime.hip server_post): the gate waits until the
+// frame's ring-slot count reaches `target` (one wave; sc1 polls with a sleep, bounded: after `timeout_ticks` it
+// records the failure in the host-visible error word and returns), then the blend reads the frame's colours with sc1
+// loads (written through by the server's waves) and blends them into the accumulator: acc*(1-w) + c*w, w = 1/FrameCount
+// (AccumulationShader.shader:33), the same operations as every other blend.  Both fit beside the server's waves
+// (64-thread groups, no LDS, few registers).
+__global__ __launch_bounds__(64) void hg_server_gate(const uint32_t* __restrict__ done, uint32_t target,
+                                                     uint64_t timeout_ticks, unsigned long long* __restrict__ err) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        if (spin < 256u) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(8);
+    }
+}
+__global__ __launch_bounds__(64) void hg_server_blend(float4* __restrict__ acc, const float4* __restrict__ colors,
+                                                      uint32_t n_slots, int32_t frame_count) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n_slots) return;
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(colors + i);
+    const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float4 c = make_float4(__uint_as_float(uint32_t(lo)), __uint_as_float(uint32_t(lo >> 32)),
+                                 __uint_as_float(uint32_t(hi)), __uint_as_float(uint32_t(hi >> 32)));
+    float4 a = acc[i];
+    const float w = rcp_exact(float(uint32_t(frame_count)));
+    const float k = 1.0f - w;
+    a = make_float4(a.x * k + c.x * w, a.y * k + c.y * w, a.z * k + c.z * w, a.w * k + 1.0f * w);
+    acc[i] = a;
+}
+hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_slots, int32_t frame_count,
+                                  const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
+                                  unsigned long long* err, hipStream_t stream) {
+    hipLaunchKernelGGL(hg_server_gate, dim3(1), dim3(64), 0, stream, done, target, timeout_ticks, err);
+    if (n_slots)
+        hipLaunchKernelGGL(hg_server_blend, dim3((n_slots + 63) / 64), dim3(64), 0, stream, acc, colors, n_slots,
+                           frame_count);
     return hipGetLastError();
 }
 

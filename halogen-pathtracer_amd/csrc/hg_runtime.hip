@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -28,30 +29,15 @@
 
 hipError_t hg_launch_mega(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
 hipError_t hg_launch_mega_regen(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
-hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream);
+hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool counters, hipStream_t stream,
+                                 bool server = false);
+hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_slots, int32_t frame_count,
+                                  const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
+                                  unsigned long long* err, hipStream_t stream);
 hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
 hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, void* scratch,
                                  unsigned long long* faults, hipStream_t stream);
 size_t hg_order_scratch_bytes(uint32_t n);
-#ifndef HG_WITH_VARIANTS
-#define HG_WITH_VARIANTS 0  // A/B variants (wavefront pipeline, path pool): make VARIANTS=1
-#endif
-#if HG_WITH_VARIANTS
-hipError_t hg_launch_mega_pool(const HgKernelParams& kp, bool counters, hipStream_t stream);
-uint32_t hg_pool_slots();
-uint32_t hg_pool_tiles();
-hipError_t hg_wf_launch_gen(const HgKernelParams& kp, uint32_t* q_out, uint32_t* n_out, hipStream_t s);
-hipError_t hg_wf_launch_trace(const HgKernelParams& kp, int grid, int block, bool counters, const uint32_t* q_in,
-                              const uint32_t* n_in, uint32_t* head, hipStream_t s);
-hipError_t hg_wf_launch_shade(const HgKernelParams& kp, int grid, const uint32_t* q_in, const uint32_t* n_in,
-                              uint32_t* q_out, uint32_t* n_out, hipStream_t s);
-int hg_wf_trace_blocks_per_cu(int block, size_t lds_bytes);
-size_t hg_wf_trace_lds_bytes(uint32_t stack_depth, int block);
-#else  // never reached: hg_set_option refuses the variants in this build
-static hipError_t hg_launch_mega_pool(const HgKernelParams&, bool, hipStream_t) { return hipErrorNotSupported; }
-static uint32_t hg_pool_slots() { return 1; }
-static uint32_t hg_pool_tiles() { return 1; }
-#endif
 int64_t hg_selftest_rcp_all(int64_t* tested);
 
 namespace {
@@ -107,7 +93,7 @@ float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); 
 float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 float bits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
-// Padded world-space boxes of a mesh root's two children (for the exact mesh skip in hg_wavefront.hip).
+// Padded world-space boxes of a mesh root's two children (for the exact mesh skip, hg_device.h mesh_live_mask).
 // The local box corners go through the double-precision inverse of the float worldToLocal the kernel uses;
 // the pad (1e-3 of the box size + 1e-4 of the coordinate magnitude + 1e-5) exceeds by orders of magnitude
 // the float rounding of the reference's local-space slab test (~1e-7 relative), so "misses the padded box"
@@ -183,78 +169,12 @@ bool mesh_cull_boxes(const hg_mat4& w2l, const BVHEntry& A, const BVHEntry& B, H
     return world_box(l2w, A, dm.cull_a_lo, dm.cull_a_hi) && world_box(l2w, B, dm.cull_b_lo, dm.cull_b_hi);
 }
 
-// Hot-node prefix (HG_NODE_CACHE > 0): renumber the device records so that the first `k` are the top of every
-// mesh's BLAS in breadth-first order (all meshes' roots, then their inner children, level by level; a node's two
-// child records stay adjacent), the records every traversal starts with.  The streaming kernel copies records
-// [0, hot) into LDS per wave and serves node fetches below `hot` from there.  Traversal follows refs, so the
-// numbering changes no visit order or result.  Returns the number of hot records.
-uint32_t ubits(float f) {
-    uint32_t u;
-    std::memcpy(&u, &f, 4);
-    return u;
-}
-
-// The child-pair record layout (hg_device.h node_pair): where child 0 / 1's ref lives, and the writer
-float& pair_ref_slot(float4* r, int child) {
-#if HG_PAIR_SOA
-    return child == 0 ? r[3].x : r[3].y;
-#else
-    return child == 0 ? r[0].w : r[1].w;
-#endif
-}
+// The child-pair record layout (hg_device.h node_pair): q0 = (A.lo, refA), q1 = (A.hi, refB), q2 = (B.lo, -), q3 = (B.hi, -)
 void put_pair(float4* r, const BVHEntry& A, const BVHEntry& B, uint32_t ra, uint32_t rb) {
-#if HG_PAIR_SOA
-    r[0] = f4(A.boundingCornerA.x, B.boundingCornerA.x, A.boundingCornerA.y, B.boundingCornerA.y);
-    r[1] = f4(A.boundingCornerA.z, B.boundingCornerA.z, A.boundingCornerB.x, B.boundingCornerB.x);
-    r[2] = f4(A.boundingCornerB.y, B.boundingCornerB.y, A.boundingCornerB.z, B.boundingCornerB.z);
-    r[3] = f4(bits(ra), bits(rb), 0.0f, 0.0f);
-#else
     r[0] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z, bits(ra));
     r[1] = f4(A.boundingCornerB.x, A.boundingCornerB.y, A.boundingCornerB.z, bits(rb));
     r[2] = f4(B.boundingCornerA.x, B.boundingCornerA.y, B.boundingCornerA.z, 0.0f);
     r[3] = f4(B.boundingCornerB.x, B.boundingCornerB.y, B.boundingCornerB.z, 0.0f);
-#endif
-}
-
-uint32_t hot_prefix(std::vector<float4>& rec, std::vector<HgDevMesh>& dm, uint32_t k) {
-    const uint32_t n = uint32_t(rec.size() / 4);
-    k = std::min(k, n);
-    if (k == 0) return 0;
-    std::vector<uint32_t> newi(n, HG_NONE);
-    std::vector<uint32_t> queue;
-    uint32_t next = 0;
-    for (const HgDevMesh& m : dm)
-        if (!(m.root_ref & HG_LEAF_BIT) && m.root_ref < n && newi[m.root_ref] == HG_NONE && next < k) {
-            newi[m.root_ref] = next++;
-            queue.push_back(m.root_ref);
-        }
-    for (size_t q = 0; q < queue.size() && next < k; ++q) {
-        const uint32_t r = queue[q];
-        for (int child = 0; child < 2 && next < k; ++child) {
-            const uint32_t ref = ubits(pair_ref_slot(&rec[4 * size_t(r)], child));
-            if ((ref & HG_LEAF_BIT) || ref >= n || newi[ref] != HG_NONE) continue;
-            newi[ref] = next++;
-            queue.push_back(ref);
-        }
-    }
-    const uint32_t hot = next;
-    for (uint32_t r = 0; r < n; ++r)
-        if (newi[r] == HG_NONE) newi[r] = next++;
-    std::vector<float4> out(rec.size());
-    auto remap = [&](uint32_t ref) { return (ref & HG_LEAF_BIT) || ref >= n ? ref : newi[ref]; };
-    for (uint32_t r = 0; r < n; ++r) {
-        float4* dst = &out[4 * size_t(newi[r])];
-        const float4* src = &rec[4 * size_t(r)];
-        dst[0] = src[0];
-        dst[1] = src[1];
-        dst[2] = src[2];
-        dst[3] = src[3];
-        for (int child = 0; child < 2; ++child)
-            pair_ref_slot(dst, child) = bits(remap(ubits(pair_ref_slot(const_cast<float4*>(src), child))));
-    }
-    rec.swap(out);
-    for (HgDevMesh& m : dm) m.root_ref = remap(m.root_ref);
-    return hot;
 }
 
 // fn(begin, end) over [0, n) in contiguous chunks on the persistent host pool (hg_host_pool.h), at most `max_threads`
@@ -347,9 +267,51 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     return HG_OK;
 }
 
+double host_seconds() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- the render server (hg_ctx::Server; device side hg_mega.hip kServer) ------------------------------------------
+// A server idle this long (no frame posted) is restarted instead of posted to: its waves leave after
+// kServerIdleTicks without work, and a post must never meet a server whose waves are leaving (a wave's idle time is at
+// most the host's time since its last post, checked just before each post, and a tenth of theirs).
+constexpr double kServerIdleS = 0.020;
+constexpr uint32_t kServerIdleTicks = 20000000u;           // 200 ms of the 100-MHz s_memrealtime
+constexpr uint64_t kGateTimeoutTicks = 30ull * 100000000ull;  // a frame's gate gives up after 30 s (reported)
+
+// A gate's timeout (the frame's count never reached its target) reported once, as an error of the entry point
+int server_check(hg_ctx* c) {
+    if (c->sv.host && __atomic_load_n(&c->sv.host[1], __ATOMIC_SEQ_CST)) {
+        __atomic_store_n(&c->sv.host[1], 0ull, __ATOMIC_SEQ_CST);
+        return fail(c, HG_E_HIP, "render server: a frame's gate timed out (its trace never completed)");
+    }
+    return HG_OK;
+}
+
+// Stop the server: set the stop flag, the waves drain every frame posted and leave; wait (bounded) for the kernel.
+int server_stop(hg_ctx* c) {
+    hg_ctx::Server& S = c->sv;
+    if (!S.running) return HG_OK;
+    __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted) | HG_SV_STOP, __ATOMIC_SEQ_CST);
+    const double t0 = host_seconds();
+    hipError_t q;
+    while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
+        if (host_seconds() - t0 > 60.0) {
+            (void)hipGetLastError();
+            return fail(c, HG_E_HIP, "render server did not stop within 60 s");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    (void)hipGetLastError();  // hipErrorNotReady is a status here
+    S.running = false;
+    if (q != hipSuccess) return fail(c, HG_E_HIP, "render server: %s", hipGetErrorString(q));
+    return server_check(c);
+}
+
 // Wait for every stream of the context: the context stream and both trace streams (before device buffers that a
-// trace in flight may read are changed or freed)
+// trace in flight may read are changed or freed); the render server is stopped first
 int quiesce(hg_ctx* c) {
+    if (int rc = server_stop(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (c->rb_stream) HG_HIP(c, hipStreamSynchronize(c->rb_stream));
     for (hg_ctx::TraceLane& L : c->lanes)
@@ -376,19 +338,6 @@ int alloc_target(hg_ctx* c) {
         L.frames_since_order = 0;
     }
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
-    const size_t slots = size_t(c->n_local_tiles) * 64;
-#if HG_WITH_VARIANTS  // wavefront pipeline path state (152 B per pixel slot)
-    for (DevBuf* b : {&c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col, &c->wf_sum, &c->wf_tuvo})
-        if (int rc = ensure(c, *b, slots * sizeof(float4))) return rc;
-    for (DevBuf* b : {&c->wf_st, &c->wf_st2})
-        if (int rc = ensure(c, *b, slots * sizeof(uint4))) return rc;
-    for (DevBuf* b : {&c->wf_ms, &c->wf_id})
-        if (int rc = ensure(c, *b, slots * sizeof(uint2))) return rc;
-    for (DevBuf* b : {&c->wf_q0, &c->wf_q1})
-        if (int rc = ensure(c, *b, slots * sizeof(uint32_t))) return rc;
-#else
-    (void)slots;
-#endif
     c->rb_pending = 0;  // quiesced: begun readbacks are complete, and their images die with the old size or tiling
     c->rb_next = 0;
     release(c->acc);
@@ -402,84 +351,6 @@ int alloc_target(hg_ctx* c) {
 }
 
 
-#if HG_WITH_VARIANTS
-// The bounce loop of the wavefront pipeline: gen, then (trace, shade) per iteration until the queue is empty.
-// The host does not wait for queue lengths: it launches ahead and polls pinned copies of the lengths a few
-// iterations behind, stopping once one of them reads zero (an empty queue stays empty).
-int render_wavefront(hg_ctx* c, const HgKernelParams& kp) {
-    const uint64_t max_iter64 = uint64_t(kp.n_frames) * kp.spp * (uint64_t(kp.max_bounces) + 1u);
-    if (max_iter64 > (1ull << 30)) return fail(c, HG_E_UNSUPPORTED, "n_frames * spp * (maxBounces+1) too large");
-    const size_t L = size_t(max_iter64);
-    if (int rc = ensure(c, c->wf_counts, (L + 1) * sizeof(uint32_t))) return rc;
-    if (int rc = ensure(c, c->wf_heads, L * sizeof(uint32_t))) return rc;
-    const size_t n_polls = L / 4 + 2;
-    if (c->poll_cap < n_polls) {
-        if (c->poll_host) (void)hipHostFree(c->poll_host);
-        c->poll_host = nullptr;
-        HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->poll_host), n_polls * sizeof(uint32_t), 0));
-        c->poll_cap = n_polls;
-    }
-    while (c->poll_events.size() < 8) {
-        hipEvent_t e;
-        HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->poll_events.push_back(e);
-    }
-    uint32_t* counts = static_cast<uint32_t*>(c->wf_counts.p);
-    uint32_t* heads = static_cast<uint32_t*>(c->wf_heads.p);
-    uint32_t* q[2] = {static_cast<uint32_t*>(c->wf_q0.p), static_cast<uint32_t*>(c->wf_q1.p)};
-    HG_HIP(c, hipMemsetAsync(counts, 0, (L + 1) * sizeof(uint32_t), c->stream));
-    HG_HIP(c, hipMemsetAsync(heads, 0, L * sizeof(uint32_t), c->stream));
-    hipError_t e = hg_wf_launch_gen(kp, q[0], counts, c->stream);
-    if (e != hipSuccess) return fail(c, HG_E_HIP, "gen launch failed: %s", hipGetErrorString(e));
-
-    const int block = c->block;
-    const size_t lds = hg_wf_trace_lds_bytes(kp.stack_depth, block);
-    const int bpc = hg_wf_trace_blocks_per_cu(block, lds);
-    const int trace_grid = std::max(1, bpc * c->n_cu);
-    HgKernelParams kpt = kp;
-    kpt.spill_stride = uint32_t(trace_grid) * uint32_t(block);
-    if (kp.stack_depth > HG_LDS_STACK) {
-        if (int rc = ensure(c, c->wf_spill, size_t(kpt.spill_stride) * (kp.stack_depth - HG_LDS_STACK) * 4)) return rc;
-        kpt.spill = static_cast<uint32_t*>(c->wf_spill.p);
-    }
-    const int shade_grid = int(std::max<size_t>(1, std::min<size_t>((kp.n_slots + 255) / 256, size_t(c->n_cu) * 8)));
-    const size_t POLL = 4;  // poll every 4 iterations, read back two polls behind
-    size_t polls = 0;
-    for (size_t it = 0; it < L; ++it) {
-        std::pair<hipEvent_t, hipEvent_t> tev;
-        if (c->timing) {
-            if (int rc = event_pair(c, tev)) return rc;
-            HG_HIP(c, hipEventRecord(tev.first, c->stream));
-        }
-        e = hg_wf_launch_trace(kpt, trace_grid, block, kp.counters != nullptr, q[it & 1], counts + it, heads + it,
-                               c->stream);
-        if (e != hipSuccess) return fail(c, HG_E_HIP, "trace launch failed: %s", hipGetErrorString(e));
-        if (c->timing) {
-            HG_HIP(c, hipEventRecord(tev.second, c->stream));
-            c->pending_trace.push_back(tev);
-        }
-        e = hg_wf_launch_shade(kp, shade_grid, q[it & 1], counts + it, q[(it + 1) & 1], counts + it + 1, c->stream);
-        if (e != hipSuccess) return fail(c, HG_E_HIP, "shade launch failed: %s", hipGetErrorString(e));
-        if (it % POLL == POLL - 1 && it + 1 < L) {
-            HG_HIP(c, hipMemcpyAsync(c->poll_host + polls, counts + it + 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                     c->stream));
-            HG_HIP(c, hipEventRecord(c->poll_events[polls % c->poll_events.size()], c->stream));
-            ++polls;
-            if (polls >= 3) {  // check the poll issued two polls ago (normally complete by now)
-                const size_t k = polls - 3;
-                hipEvent_t pe = c->poll_events[k % c->poll_events.size()];
-                if (hipEventQuery(pe) == hipSuccess && c->poll_host[k] == 0) break;
-            }
-        }
-    }
-    return HG_OK;
-}
-#else
-int render_wavefront(hg_ctx* c, const HgKernelParams&) {
-    return fail(c, HG_E_UNSUPPORTED, "wavefront pipeline not built (make VARIANTS=1)");
-}
-#endif
-
 }  // namespace
 
 extern "C" {
@@ -488,8 +359,7 @@ namespace {
 // A trace stream (HG_LANE_STREAMS).  Plain streams share HIP's pool of GPU_MAX_HW_QUEUES (4) hardware queues with every
 // other stream of the process; two trace streams on one queue serialise their launches.
 hipError_t create_lane_stream(const hg_ctx* c, int lane, hipStream_t* s) {
-#if HG_LANE_STREAMS == 1 || HG_LANE_STREAMS == 3
-    if (HG_LANE_STREAMS == 3 && lane < HG_TRACE_LANES_BIG) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (lane < HG_TRACE_LANES_BIG) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     std::vector<uint32_t> mask(size_t((c->n_cu + 31) / 32), 0u);
     for (int i = 0; i < c->n_cu; ++i) mask[size_t(i) / 32] |= 1u << (i % 32);
     // (CU-masked streams are blocking with respect to the legacy null stream, unlike the plain ones.)  Where the
@@ -497,16 +367,6 @@ hipError_t create_lane_stream(const hg_ctx* c, int lane, hipStream_t* s) {
     if (hipExtStreamCreateWithCUMask(s, uint32_t(mask.size()), mask.data()) == hipSuccess) return hipSuccess;
     (void)hipGetLastError();
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-#elif HG_LANE_STREAMS == 2
-    (void)lane;
-    int lo = 0, hi = 0;
-    if (hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi)) return e;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-#else
-    (void)c;
-    (void)lane;
-    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-#endif
 }
 }  // namespace
 
@@ -553,13 +413,21 @@ void hg_destroy(hg_ctx* c) {
     if (!c) return;
     c->pending_frames = 0;  // held frames are discarded: nothing can observe them after this call
     (void)hipSetDevice(c->device);
+    (void)server_stop(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (hg_ctx::TraceLane& L : c->lanes)
         if (L.stream) (void)hipStreamSynchronize(L.stream);
-    for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tri_a, &c->tri_b, &c->tri_c,
-                      &c->normals, &c->cube, &c->acc, &c->counters_dev, &c->timeline, &c->wf_o, &c->wf_d, &c->wf_thr, &c->wf_col,
-                      &c->wf_sum, &c->wf_st, &c->wf_st2, &c->wf_ms, &c->wf_tuvo, &c->wf_id, &c->wf_q0, &c->wf_q1,
-                      &c->wf_counts, &c->wf_heads, &c->wf_spill, &c->pool})
+    {
+        hg_ctx::Server& S = c->sv;
+        if (S.stream) (void)hipStreamSynchronize(S.stream);
+        for (DevBuf* b : {&S.ctl, &S.done, &S.ring, &S.spill, &S.tile_cost, &S.tile_order, &S.order_scratch}) release(*b);
+        for (hipEvent_t& e : S.blended)
+            if (e) (void)hipEventDestroy(e);
+        if (S.host) (void)hipHostFree(S.host);
+        if (S.stream) (void)hipStreamDestroy(S.stream);
+    }
+    for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tris, &c->normals, &c->cube,
+                      &c->acc, &c->counters_dev, &c->spill})
         release(*b);
     for (hg_ctx::TraceLane& L : c->lanes) {
         for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.order_scratch, &L.queue})
@@ -577,8 +445,6 @@ void hg_destroy(hg_ctx* c) {
         if (c->image_copied[k]) (void)hipEventDestroy(c->image_copied[k]);
     }
     if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
-    if (c->poll_host) (void)hipHostFree(c->poll_host);
-    for (hipEvent_t e : c->poll_events) (void)hipEventDestroy(e);
     for (auto& pr : c->pending_trace) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->free_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -591,6 +457,14 @@ const char* hg_last_error(const hg_ctx* c) { return c ? c->err.c_str() : "null c
 int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, const HalogenMeshData* meshes,
                     int32_t n_meshes, const PackedHalogenMaterial* materials, int32_t n_materials,
                     const HalogenTriangle* tris, int32_t n_tris, const BVHEntry* blas, int32_t n_nodes) {
+    return hg_upload_scene_gen(c, 0, spheres, n_spheres, meshes, n_meshes, materials, n_materials, tris, n_tris, blas,
+                               n_nodes);
+}
+
+int hg_upload_scene_gen(hg_ctx* c, uint64_t geometry_generation, const HalogenSphere* spheres, int32_t n_spheres,
+                        const HalogenMeshData* meshes, int32_t n_meshes, const PackedHalogenMaterial* materials,
+                        int32_t n_materials, const HalogenTriangle* tris, int32_t n_tris, const BVHEntry* blas,
+                        int32_t n_nodes) {
     if (!c) return HG_E_INVALID;
     if (int rc = hg_ctx_flush(c)) return rc;
     if (n_spheres < 0 || n_meshes < 0 || n_materials < 0 || n_tris < 0 || n_nodes < 0)
@@ -613,13 +487,18 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
                                 size_t(n_materials) * sizeof(PackedHalogenMaterial),
                                 size_t(n_tris) * sizeof(HalogenTriangle), size_t(n_nodes) * sizeof(BVHEntry)};
     bool same[5] = {false, false, false, false, false};
+    // A caller-kept geometry generation equal to the last upload's vouches for the triangles and BVH entries (the C# /
+    // C++ / Python passes bump it when RayTracingManager's mesh registry changes): no compare of those 78 MB (C3).
+    const bool vouched = c->has_scene && geometry_generation != 0 && geometry_generation == c->geometry_gen;
     if (c->has_scene) {
         for (int k = 0; k < 5; ++k) same[k] = c->scene_copy[k].size() == bytes_in[k];
         for (int k = 0; k < 3; ++k)
             same[k] = same[k] && (!bytes_in[k] || !std::memcmp(c->scene_copy[k].data(), src[k], bytes_in[k]));
-        for (int k = 3; k < 5; ++k) same[k] = same[k] && same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]);
+        for (int k = 3; k < 5; ++k)
+            same[k] = same[k] && (vouched || same_bytes(c->scene_copy[k].data(), src[k], bytes_in[k]));
         if (same[0] && same[1] && same[2] && same[3] && same[4]) {
             c->scene_uploads_skipped++;
+            c->scene_uploads_vouched += vouched ? 1u : 0u;
             return HG_OK;
         }
     }
@@ -685,6 +564,8 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
         c->dev_meshes.swap(dm);
         c->scene_uploads++;
         c->scene_uploads_partial++;
+        c->scene_uploads_vouched += vouched ? 1u : 0u;
+        c->geometry_gen = geometry_generation;
         c->n_spheres = n_spheres;
         c->n_meshes = n_meshes;
         c->n_materials = n_materials;
@@ -698,26 +579,15 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
 
     // ---- triangles (independent per triangle: parallel)
     const size_t nt = size_t(n_tris);
-#if HG_TRI_AOS
-    std::vector<float> t9(nt * 9);  // (a, b, c) of tri_load, packed per triangle
-#else
-    std::vector<float4> ta(nt), tb(nt);
-    std::vector<float> tc(nt);
-#endif
+    std::vector<float> t9(nt * 9);  // (v0, e1, e2) of tri_load, packed per triangle
     std::vector<float4> nrm(nt * 3);
     parallel_for(nt, 32768, kHostThreads, [&](size_t lo, size_t hi) {
         for (size_t t = lo; t < hi; ++t) {
             const HalogenTriangle& h = tris[t];
             const float e1x = h.pointB.x - h.pointA.x, e1y = h.pointB.y - h.pointA.y, e1z = h.pointB.z - h.pointA.z;
             const float e2x = h.pointC.x - h.pointA.x, e2y = h.pointC.y - h.pointA.y, e2z = h.pointC.z - h.pointA.z;
-#if HG_TRI_AOS
             const float v[9] = {h.pointA.x, h.pointA.y, h.pointA.z, e1x, e1y, e1z, e2x, e2y, e2z};
             std::memcpy(&t9[9 * t], v, sizeof v);
-#else
-            ta[t] = f4(h.pointA.x, h.pointA.y, h.pointA.z, e1x);
-            tb[t] = f4(e1y, e1z, e2x, e2y);
-            tc[t] = e2z;
-#endif
             nrm[3 * t] = f4(h.normalA.x, h.normalA.y, h.normalA.z, 0.0f);
             nrm[3 * t + 1] = f4(h.normalB.x - h.normalA.x, h.normalB.y - h.normalA.y, h.normalB.z - h.normalA.z, 0.0f);
             nrm[3 * t + 2] = f4(h.normalC.x - h.normalA.x, h.normalC.y - h.normalA.y, h.normalC.z - h.normalA.z, 0.0f);
@@ -825,7 +695,6 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
         return fail(c, HG_E_UNSUPPORTED, "BLAS too large: %zu device node records", rec.size() / 4);
     if (rec.empty()) new_record();
     if (leaf.empty()) leaf.push_back(make_uint2(0, 0));
-    c->hot_records = hot_prefix(rec, dm, HG_NODE_CACHE);
     c->stack_depth = std::max<uint32_t>(2u, (max_depth + 2 + 1) & ~1u);
 
     int rc;
@@ -834,18 +703,13 @@ int hg_upload_scene(hg_ctx* c, const HalogenSphere* spheres, int32_t n_spheres, 
     if ((rc = upload(c, c->meshes, dm.data(), dm.size() * sizeof(HgDevMesh)))) return rc;
     if ((rc = upload(c, c->nodes, rec.data(), rec.size() * sizeof(float4)))) return rc;
     if ((rc = upload(c, c->leaves, leaf.data(), leaf.size() * sizeof(uint2)))) return rc;
-#if HG_TRI_AOS
-    if ((rc = upload(c, c->tri_a, t9.data(), t9.size() * sizeof(float)))) return rc;
-#else
-    if ((rc = upload(c, c->tri_a, ta.data(), ta.size() * sizeof(float4)))) return rc;
-    if ((rc = upload(c, c->tri_b, tb.data(), tb.size() * sizeof(float4)))) return rc;
-    if ((rc = upload(c, c->tri_c, tc.data(), tc.size() * sizeof(float)))) return rc;
-#endif
+    if ((rc = upload(c, c->tris, t9.data(), t9.size() * sizeof(float)))) return rc;
     if ((rc = upload(c, c->normals, nrm.data(), nrm.size() * sizeof(float4)))) return rc;
     // the retained copies the next upload compares against (while the device copies run)
     for (int k = 0; k < 5; ++k) copy_bytes(c->scene_copy[k], src[k], bytes_in[k]);
     c->dev_meshes = dm;
     HG_HIP(c, hipStreamSynchronize(c->stream));  // host staging vectors die at return
+    c->geometry_gen = geometry_generation;
     c->scene_uploads++;
     c->n_spheres = n_spheres;
     c->n_meshes = n_meshes;
@@ -938,6 +802,186 @@ int render_check(hg_ctx* c, int32_t n_frames) {
     return HG_OK;
 }
 
+// The server can take the frame of FrameCount `fc` next: running, started with these parameters and options, `fc`
+// continuing its chain, room left in its lifetime's unit numbering, not idle for long and its kernel still resident
+bool server_continues(hg_ctx* c, int32_t fc) {
+    const hg_ctx::Server& S = c->sv;
+    if (!S.running) return false;
+    hg_params p = c->params;
+    p.frameCount = S.params.frameCount;
+    if (std::memcmp(&p, &S.params, sizeof p) != 0 || int64_t(fc) != int64_t(S.params.frameCount) + int64_t(S.posted) ||
+        S.kernel_variant != c->kernel || S.descent_t != c->descent_t || S.posted >= S.cap ||
+        host_seconds() - S.last_post_s >= kServerIdleS)
+        return false;
+    const hipError_t q = hipStreamQuery(S.stream);
+    (void)hipGetLastError();
+    return q == hipErrorNotReady;
+}
+
+// Launch the server for the frames from FrameCount `fc`: kp is the launch's parameter block as render_now built it.  HG_E_UNSUPPORTED when the device gives no stream with a hardware queue of its own (the server's
+// gates on the context stream must never queue behind it): the caller launches per call instead.
+int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
+    hg_ctx::Server& S = c->sv;
+    if (!S.stream) {
+        std::vector<uint32_t> mask(size_t((c->n_cu + 31) / 32), 0u);
+        for (int i = 0; i < c->n_cu; ++i) mask[size_t(i) / 32] |= 1u << (i % 32);
+        if (hipExtStreamCreateWithCUMask(&S.stream, uint32_t(mask.size()), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            S.stream = nullptr;
+            c->server_on = 0;
+            return HG_E_UNSUPPORTED;
+        }
+        for (hipEvent_t& e : S.blended) HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&S.host), 256, hipHostMallocMapped));
+        S.host[0] = S.host[1] = 0ull;
+    }
+    const uint32_t tiles = uint32_t(c->n_local_tiles);
+    const size_t per_frame = size_t(tiles) * 64u * sizeof(float4);
+    uint32_t ring = HG_SV_RING;
+    while (ring > 2u && size_t(ring) * per_frame > (size_t(2) << 30)) ring >>= 1;
+    const uint32_t slots = uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES;
+    const uint32_t grid = std::min(tiles, slots);
+    const uint32_t lds_part = HG_STREAM_LDS_STACK;
+    const size_t spill_bytes = kp_in.stack_depth > lds_part ? size_t(grid) * 64u * (kp_in.stack_depth - lds_part) * 4u : 0;
+    const size_t tb = size_t(tiles) * sizeof(uint32_t);
+    // the last lifetime's gates and blends on the context stream read its ring and counts: everything below runs after
+    // them (an event, no host wait) unless a buffer must move (then the context stream is drained first)
+    if (S.ring.bytes < size_t(ring) * per_frame || S.done.bytes < size_t(ring) * 128u)
+        HG_HIP(c, hipStreamSynchronize(c->stream));
+    int rc = ensure(c, S.ring, size_t(ring) * per_frame);
+    if (!rc) rc = ensure(c, S.done, size_t(ring) * 128u);
+    if (!rc) rc = ensure(c, S.ctl, HG_SV_CTL_BYTES);
+    if (!rc && spill_bytes) rc = ensure(c, S.spill, spill_bytes);
+    if (!rc && c->tile_order_on) rc = ensure(c, S.tile_cost, 2 * tb);
+    if (!rc && c->tile_order_on) rc = ensure(c, S.tile_order, tb);
+    const size_t osb = hg_order_scratch_bytes(tiles);
+    if (!rc && c->tile_order_on && S.order_scratch.bytes < osb) {
+        rc = ensure(c, S.order_scratch, osb);
+        if (!rc && hipMemsetAsync(S.order_scratch.p, 0, S.order_scratch.bytes, S.stream) != hipSuccess)
+            rc = fail(c, HG_E_HIP, "hipMemsetAsync(server order scratch) failed");
+    }
+    if (rc) return rc;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (int r = event_pair(c, ev)) return r;
+    HG_HIP(c, hipEventRecord(ev.first, c->stream));
+    HG_HIP(c, hipStreamWaitEvent(S.stream, ev.first, 0));
+    c->free_events.push_back(ev);
+    HG_HIP(c, hipMemsetAsync(S.ctl.p, 0, HG_SV_CTL_BYTES, S.stream));
+    HG_HIP(c, hipMemsetAsync(S.done.p, 0, size_t(ring) * 128u, S.stream));
+    HgKernelParams kp = kp_in;
+    kp.tile_order = nullptr;
+    kp.tile_cost = nullptr;
+    if (c->tile_order_on) {
+        kp.tile_cost = static_cast<unsigned long long*>(S.tile_cost.p);
+        if (S.tile_cost_valid) {  // the cost order of the last lifetime's frames
+            HG_HIP(c, hg_launch_order_tiles(kp.tile_cost, static_cast<uint32_t*>(S.tile_order.p), tiles, S.order_scratch.p,
+                                            static_cast<unsigned long long*>(c->counters_dev.p) + 18, S.stream));
+            kp.tile_order = static_cast<const uint32_t*>(S.tile_order.p);
+        } else {
+            HG_HIP(c, hipMemsetAsync(kp.tile_cost, 0, size_t(tiles) * sizeof(unsigned long long), S.stream));
+            S.tile_cost_valid = true;
+        }
+    }
+    kp.frame_color = static_cast<float4*>(S.ring.p);
+    kp.frames_done = static_cast<uint32_t*>(S.done.p);
+    kp.queue = static_cast<uint32_t*>(S.ctl.p);
+    kp.resident_waves = slots;
+    kp.wave_units = 1;
+    kp.spill = spill_bytes ? static_cast<uint32_t*>(S.spill.p) : nullptr;
+    kp.spill_stride = grid * 64u;
+    kp.first_frame = fc;
+    kp.n_frames = 1;
+    kp.frame_split = 1;
+    kp.accumulate = 1;
+    void* post = nullptr;
+    HG_HIP(c, hipHostGetDevicePointer(&post, S.host, 0));
+    kp.sv_post = static_cast<const unsigned long long*>(post);
+    kp.sv_ring = ring;
+    kp.sv_frames_cap = std::min<uint32_t>(1u << 24, uint32_t((uint64_t(1) << 31) / std::max<uint32_t>(tiles, 1u)));
+    kp.sv_idle_ticks = kServerIdleTicks;
+    if ((tiles & (tiles - 1u)) == 0u) {  // unit -> frame (hg_mega.hip sv_frame): a shift, or a multiply-high and a shift
+        kp.sv_div_magic = 0u;
+        kp.sv_div_shift = uint32_t(__builtin_ctz(tiles));
+    } else {
+        const uint32_t l = 31u - uint32_t(__builtin_clz(tiles));
+        kp.sv_div_magic = uint32_t(((uint64_t(1) << (32 + l)) + tiles - 1u) / tiles);
+        kp.sv_div_shift = l;
+    }
+    __atomic_store_n(&S.host[0], 0ull, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&S.host[1], 0ull, __ATOMIC_SEQ_CST);
+    HG_HIP(c, hg_launch_mega_stream(kp, 64, c->counters_on != 0, S.stream, true));
+    S.running = true;
+    S.ring_n = ring;
+    S.posted = 0;
+    S.cap = kp.sv_frames_cap;
+    for (uint32_t k = 0; k < HG_SV_RING; ++k) {
+        S.uses[k] = 0;
+        S.blend_valid[k] = false;
+    }
+    S.params = c->params;
+    S.params.frameCount = fc;
+    S.kernel_variant = c->kernel;
+    S.descent_t = c->descent_t;
+    S.kp = kp;
+    S.last_post_s = host_seconds();
+    c->server_launches++;
+    return HG_OK;
+}
+
+// Post the next frame to the server: its gate + blend on the context stream (in frame order, like every other blend),
+// then the post word.  Frames run at most ring_n ahead of their blends (the host waits for the blend of the frame
+// ring_n back before reusing its ring slot); HG_E_UNSUPPORTED (nothing posted) when that wait left the server idle too
+// long to post to.
+int server_post(hg_ctx* c) {
+    hg_ctx::Server& S = c->sv;
+    const uint32_t k = S.posted, s = k & (S.ring_n - 1u);
+    if (S.blend_valid[s]) {
+        HG_HIP(c, hipEventSynchronize(S.blended[s]));
+        if (host_seconds() - S.last_post_s >= kServerIdleS) return HG_E_UNSUPPORTED;
+    }
+    S.uses[s]++;
+    const uint32_t tiles = uint32_t(c->n_local_tiles), n_slots = tiles * 64u;
+    void* err = nullptr;
+    HG_HIP(c, hipHostGetDevicePointer(&err, S.host + 1, 0));
+    HG_HIP(c, hg_launch_server_frame(static_cast<float4*>(c->acc.p),
+                                     static_cast<const float4*>(S.ring.p) + size_t(s) * n_slots, n_slots,
+                                     S.kp.first_frame + int32_t(k), static_cast<const uint32_t*>(S.done.p) + 32u * s,
+                                     S.uses[s] * tiles, kGateTimeoutTicks, static_cast<unsigned long long*>(err),
+                                     c->stream));
+    HG_HIP(c, hipEventRecord(S.blended[s], c->stream));
+    S.blend_valid[s] = true;
+    S.posted = k + 1u;
+    __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted), __ATOMIC_SEQ_CST);
+    S.last_post_s = host_seconds();
+    c->server_frames++;
+    return HG_OK;
+}
+
+// n_frames frames from FrameCount = params.frameCount through the server (started or restarted as needed).  A first
+// HG_E_UNSUPPORTED (no stream of its own) falls back to launches; nothing was posted then.
+int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
+    if (int rc = server_check(c)) return rc;
+    for (int32_t f = 0; f < n_frames; ++f) {
+        const int32_t fc = c->params.frameCount + f;
+        for (int attempt = 0;; ++attempt) {
+            if (c->sv.running && !server_continues(c, fc))
+                if (int rc = server_stop(c)) return rc;
+            if (!c->sv.running) {
+                const int rc = server_start(c, kp, fc);
+                if (rc == HG_E_UNSUPPORTED && f > 0) return fail(c, HG_E_HIP, "render server: restart failed");
+                if (rc) return rc;
+            }
+            const int rc = server_post(c);
+            if (rc != HG_E_UNSUPPORTED) {
+                if (rc) return rc;
+                break;
+            }
+            if (attempt) return fail(c, HG_E_HIP, "render server: a fresh server refused a post");
+        }
+    }
+    return HG_OK;
+}
+
 // One launch of n_frames frames from FrameCount = params.frameCount (which it advances when accumulating)
 int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (!c->has_scene) return fail(c, HG_E_NOSCENE, "hg_upload_scene not called");
@@ -992,11 +1036,6 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.n_ranks = c->n_ranks;
     kp.n_local_tiles = c->n_local_tiles;
     kp.stack_depth = c->stack_depth;
-    kp.hot_records = c->hot_records;
-    // deep BLAS (the dragon: 32 levels) descend in long, uneven runs: let the last few lanes pause while the rest
-    // test their leaves (C3 +12 % at T = 3); shallow scenes keep the classic while-while (tools/sweeps/sweep28-29.txt)
-
-    kp.refill_min = uint32_t(c->refill);
     kp.cube_size = c->cube_size;
     kp.cube_mips = c->cube_mips;
     std::memcpy(kp.cube_mip_offset, c->cube_mip_offset, sizeof kp.cube_mip_offset);
@@ -1005,25 +1044,11 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     kp.materials = static_cast<const float4*>(c->materials.p);
     kp.nodes = static_cast<const float4*>(c->nodes.p);
     kp.leaves = static_cast<const uint2*>(c->leaves.p);
-    kp.tri_a = static_cast<const float4*>(c->tri_a.p);
-    kp.tri_b = static_cast<const float4*>(c->tri_b.p);
-    kp.tri_c = static_cast<const float*>(c->tri_c.p);
+    kp.tris = static_cast<const float*>(c->tris.p);
     kp.normals = static_cast<const float4*>(c->normals.p);
     kp.cube = static_cast<const float4*>(c->cube.p);
     kp.acc = static_cast<float4*>(c->acc.p);
     kp.counters = static_cast<unsigned long long*>(c->counters_dev.p);
-
-    kp.n_slots = uint32_t(c->n_local_tiles) * 64u;
-    kp.p_o = static_cast<float4*>(c->wf_o.p);
-    kp.p_d = static_cast<float4*>(c->wf_d.p);
-    kp.p_thr = static_cast<float4*>(c->wf_thr.p);
-    kp.p_col = static_cast<float4*>(c->wf_col.p);
-    kp.p_sum = static_cast<float4*>(c->wf_sum.p);
-    kp.p_st = static_cast<uint4*>(c->wf_st.p);
-    kp.p_st2 = static_cast<uint4*>(c->wf_st2.p);
-    kp.p_ms = static_cast<uint2*>(c->wf_ms.p);
-    kp.h_tuvo = static_cast<float4*>(c->wf_tuvo.p);
-    kp.h_id = static_cast<uint2*>(c->wf_id.p);
     if (!c->counters_on) kp.counters = nullptr;
 
     std::pair<hipEvent_t, hipEvent_t> ev;
@@ -1038,21 +1063,17 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     const bool stream_auto = deep_blas || c->n_meshes >= HG_STREAM_MIN_MESHES;
     const int32_t kern = c->kernel == HG_KERNEL_AUTO ? (stream_auto ? HG_KERNEL_MEGA_STREAM : HG_KERNEL_MEGA_REGEN)
                                                      : c->kernel;
-    const bool mega = kern != HG_KERNEL_WAVEFRONT || p.halogenDebugMode != 0;
     // relaxed descent threshold: 3 for the regen / lockstep kernels, HG_STREAM_DESCENT_T for the streaming one
     kp.stream_deep = deep_blas ? 1u : 0u;
     kp.descent_t = c->descent_t >= 0 ? uint32_t(c->descent_t)
                    : !deep_blas      ? 0u
                    : kern == HG_KERNEL_MEGA_STREAM ? uint32_t(HG_STREAM_DESCENT_T)
                                                    : uint32_t(HG_DESCENT_T);
-    if (mega) {
-        const bool regen = (kern == HG_KERNEL_MEGA_REGEN || kern == HG_KERNEL_MEGA_STREAM ||
-                            kern == HG_KERNEL_MEGA_POOL) &&
-                           p.halogenDebugMode == 0 &&
+    {
+        const bool regen = (kern == HG_KERNEL_MEGA_REGEN || kern == HG_KERNEL_MEGA_STREAM) && p.halogenDebugMode == 0 &&
                            kp.max_bounces <= HG_REGEN_MAX_BOUNCES && kp.spp < HG_REGEN_MAX_CHUNK;
         // default block (option 128): 64 for the regenerating kernel (one tile per workgroup schedules best,
         // tools/sweeps/sweep12.txt), 256 for the lockstep one
-        const bool pool_k = regen && kern == HG_KERNEL_MEGA_POOL;
         // the regenerating / streaming kernels run one wave per workgroup (their LDS row layout assumes it)
         const int mblock = regen ? 64 : (c->block == 128 ? 256 : c->block);
         // Frame-parallel split: `split` waves share each tile, each tracing a chunk of the frames, so a launch has
@@ -1062,10 +1083,8 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         // rank's share at N=8 314 -> 1212.
         const bool stream_k = regen && kern == HG_KERNEL_MEGA_STREAM;
         const int64_t tiles = c->n_local_tiles;
-        // work units: one tile per wave (regen / stream), HG_POOL_TILES tiles per wave (pool)
-        const int64_t units = pool_k ? (tiles + hg_pool_tiles() - 1) / hg_pool_tiles() : tiles;
-        const int64_t resident =
-            int64_t(c->n_cu) * 4 * (pool_k ? HG_POOL_WAVES : stream_k ? HG_STREAM_WAVES : HG_MEGA_WAVES);
+        const int64_t units = tiles;  // work units: one tile per wave
+        const int64_t resident = int64_t(c->n_cu) * 4 * (stream_k ? HG_STREAM_WAVES : HG_MEGA_WAVES);
         int split = 1;
         if (regen && n_frames > 1 && tiles > 0) {
             if (c->frame_split > 0) split = std::min(n_frames, int(c->frame_split));
@@ -1086,33 +1105,48 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         // The streaming kernel (always) and the regenerating kernel (item scheduling or a frame split) store every
         // frame's colour and blend them into the accumulator in frame order afterwards (hg_blend_frames): such a launch
         // is traced on a trace stream and blended on the context stream (the trace pipeline, hg_ctx.h).
-        const bool items_k = regen && !pool_k && (stream_k || HG_REGEN_ITEMS);
-        const bool pipelined = regen && !pool_k && (items_k || split > 1);
+        const bool items_k = regen && (stream_k || HG_REGEN_ITEMS);
+        const bool pipelined = regen && (items_k || split > 1);
         const size_t per_frame = size_t(tiles) * 64 * sizeof(float4);
         if (pipelined)
             chunk_max = int(std::max<size_t>(1, std::min<size_t>(size_t(chunk_max), kFrameColorCap / per_frame)));
         const int mgrid = int((units * split + mblock / 64 - 1) / (mblock / 64));
-        if (pool_k) {
-            if (int rc = ensure(c, c->pool, size_t(mgrid) * hg_pool_slots() * 8 * sizeof(float4))) {
-                c->free_events.push_back(ev);
-                return rc;
-            }
-            kp.pool = static_cast<float4*>(c->pool.p);
-        }
         kp.spill_stride = uint32_t(mgrid) * uint32_t(mblock);
         // stack entries beyond the LDS part: one column per thread (the streaming kernel's LDS part may be shorter)
         const uint32_t lds_part = std::min<uint32_t>(HG_MEGA_LDS_STACK, HG_STREAM_LDS_STACK);
         const size_t spill_bytes =
             kp.stack_depth > lds_part ? size_t(kp.spill_stride) * (kp.stack_depth - lds_part) * 4 : 0;
         if (spill_bytes && !pipelined) {
-            if (int rc = ensure_quiet(c, c->wf_spill, spill_bytes)) {
+            if (int rc = ensure_quiet(c, c->spill, spill_bytes)) {
                 c->free_events.push_back(ev);
                 return rc;
             }
-            kp.spill = static_cast<uint32_t*>(c->wf_spill.p);
+            kp.spill = static_cast<uint32_t*>(c->spill.p);
         }
 
         c->counters.last_kernel = uint64_t(regen ? kern : HG_KERNEL_MEGA);
+        // the reference's one frame per call: posted to the render server (persistent trace waves)
+        if (c->server_on && stream_k && pipelined && accumulate && n_frames <= HG_QUEUE_MAX_FRAMES && tiles > 0) {
+            const int rc = server_render(c, kp, n_frames);
+            if (rc == HG_OK) {
+                HG_HIP(c, hipEventRecord(ev.second, c->stream));
+                c->pending.push_back(ev);
+                c->counters.launches++;
+                if (c->pending.size() + c->pending_trace.size() > 4096)
+                    if (int r = drain_events(c)) return r;
+                c->params.frameCount += n_frames;  // FrameCount++ per accumulated frame (RP:347)
+                return HG_OK;
+            }
+            if (rc != HG_E_UNSUPPORTED) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+        } else if (c->sv.running) {  // another kind of launch needs the GPU's wave slots
+            if (int rc = server_stop(c)) {
+                c->free_events.push_back(ev);
+                return rc;
+            }
+        }
         hipError_t e = hipSuccess;
         const bool ordered = pipelined && c->tile_order_on && tiles > 0;
         const size_t tb = size_t(tiles) * sizeof(uint32_t);
@@ -1139,11 +1173,7 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     if (!rc && hipMemsetAsync(L.order_scratch.p, 0, L.order_scratch.bytes, L.stream) != hipSuccess)
                         rc = fail(c, HG_E_HIP, "hipMemsetAsync(order scratch) failed");
                 }
-#if HG_PATH_MIGRATE
-                const size_t qbytes = HG_QUEUE_BYTES_MIG(uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES);
-#else
                 const size_t qbytes = HG_QUEUE_BYTES;
-#endif
                 if (!rc && stream_k && L.queue.bytes < qbytes) {
                     rc = ensure_quiet(c, L.queue, qbytes);
                     if (!rc && hipMemsetAsync(L.queue.p, 0, L.queue.bytes, L.stream) != hipSuccess)
@@ -1206,19 +1236,6 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                     const int64_t auto_wu = std::min<int64_t>(HG_WAVE_UNITS_MAX, tiles / (int64_t(HG_WAVE_UNITS_ROUNDS) * slots));
                     kc.wave_units = uint32_t(c->wave_units > 0 ? c->wave_units : std::max<int64_t>(1, auto_wu));
                 }
-                kc.timeline = nullptr;
-#if HG_WAVE_TIMELINE
-                if (kc.queue) {
-                    const size_t per = size_t(HG_TIMELINE_WAVES) * 4u * sizeof(unsigned long long);
-                    if (!c->timeline.p && ensure_quiet(c, c->timeline, per * HG_TIMELINE_LAUNCHES) == HG_OK)
-                        (void)hipMemset(c->timeline.p, 0, c->timeline.bytes);
-                    if (c->timeline.p) {
-                        kc.timeline = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->timeline.p) +
-                                                                          per * (c->timeline_launches++ % HG_TIMELINE_LAUNCHES));
-                        (void)hipMemsetAsync(kc.timeline, 0, per, L.stream);  // rows of waves this launch lacks
-                    }
-                }
-#endif
                 kc.tile_order = nullptr;
                 kc.tile_cost = ordered ? static_cast<unsigned long long*>(L.tile_cost.p) : nullptr;
                 // this stream's buffers are free once the blend of its previous chunk has read them
@@ -1268,14 +1285,13 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 L.blend_pending = e == hipSuccess;
                 done += kc.n_frames;
             }
-        } else if (regen) {  // the path pool, or a regenerating launch that blends in the kernel: on the context stream
+        } else if (regen) {  // a regenerating launch that blends in the kernel (make noitems): on the context stream
             HgKernelParams kc = kp;
             for (int done = 0; done < n_frames && e == hipSuccess;) {
                 kc.n_frames = std::min(n_frames - done, chunk_max);
                 kc.first_frame = accumulate ? kp.first_frame + done : 1;
                 kc.frame_split = std::min(split, kc.n_frames);
-                e = pool_k ? hg_launch_mega_pool(kc, c->counters_on != 0, c->stream)
-                           : hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
+                e = hg_launch_mega_regen(kc, mblock, c->counters_on != 0, c->stream);
                 done += kc.n_frames;
             }
         } else {
@@ -1284,12 +1300,6 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         if (e != hipSuccess) {
             c->free_events.push_back(ev);
             return fail(c, HG_E_HIP, "megakernel launch failed: %s", hipGetErrorString(e));
-        }
-    } else {
-        c->counters.last_kernel = HG_KERNEL_WAVEFRONT;
-        if (int rc = render_wavefront(c, kp)) {
-            c->free_events.push_back(ev);
-            return rc;
         }
     }
     HG_HIP(c, hipEventRecord(ev.second, c->stream));
@@ -1395,11 +1405,9 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
     // frames' blends) does not wait for the copy; else c->image, copied on the context stream
     const bool side = c->rb_side != 0;
     if (side && !c->rb_stream) {
-#if HG_RB_OWN_QUEUE  // the copy stream on a hardware queue of its own (a plain stream shares one with a trace lane)
+        // the copy stream on a hardware queue of its own (a plain stream shares one with a trace lane and waits behind
+        // its traces: depth 2 1,285 -> 1,642 Mpaths/s, sweep_r04_rbq)
         HG_HIP(c, create_lane_stream(c, HG_TRACE_LANES, &c->rb_stream));
-#else
-        HG_HIP(c, hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking));
-#endif
         for (int j = 0; j < HG_READBACK_MAX; ++j)
             HG_HIP(c, hipEventCreateWithFlags(&c->rb_untiled[j], hipEventDisableTiming));
     }
@@ -1456,6 +1464,7 @@ int hg_readback_end_data(hg_ctx* c, const void** data, size_t* n_bytes, int32_t*
     const int k = (c->rb_next - c->rb_pending + c->rb_depth) % c->rb_depth;  // the oldest begun
     HG_HIP(c, hipEventSynchronize(c->image_copied[k]));
     c->rb_pending--;
+    if (int rc = server_check(c)) return rc;
     *data = c->image_host[k];
     if (n_bytes) *n_bytes = c->image_host_bytes[k];
     if (format) *format = c->image_host_format[k];
@@ -1528,6 +1537,7 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
         if (int rc = untile_async(c, &bytes)) return rc;
         HG_HIP(c, hipMemcpyAsync(rgba, c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
         HG_HIP(c, hipStreamSynchronize(c->stream));
+        if (int rc = server_check(c)) return rc;
         return drain_events(c);
     }
     // this rank's pixels only (the others are left untouched): the tiles are repacked on the host
@@ -1596,6 +1606,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     if (!c || !out) return HG_E_INVALID;
     if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
+    if (int rc = server_stop(c)) return rc;  // (its waves add their counts when they leave)
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (int rc = drain_events(c)) return rc;
     unsigned long long v[32];
@@ -1620,6 +1631,9 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->scene_uploads = c->scene_uploads;
     out->scene_uploads_skipped = c->scene_uploads_skipped;
     out->scene_uploads_partial = c->scene_uploads_partial;
+    out->scene_uploads_vouched = c->scene_uploads_vouched;
+    out->server_launches = c->server_launches;
+    out->server_frames = c->server_frames;
     return HG_OK;
 }
 
@@ -1627,6 +1641,7 @@ int hg_reset_counters(hg_ctx* c) {
     if (!c) return HG_E_INVALID;
     if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
+    if (int rc = server_stop(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));
     if (int rc = drain_events(c)) return rc;
     HG_HIP(c, hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes));
@@ -1647,29 +1662,21 @@ int64_t hg_selftest(hg_ctx* c, int32_t test, int64_t* tested) {
     return r;
 }
 
-// Analysis builds (HG_WAVE_TIMELINE=1) only, not part of halogen_abi.h: the ring of the last HG_TIMELINE_LAUNCHES queue
-// launches' wave records (start, queue dry, end in 100-MHz ticks, items numbered), HG_TIMELINE_WAVES x 4 u64 each, and
-// how many queue launches wrote it.  tools/wave_timeline.py
-int64_t hg_debug_timeline(hg_ctx* c, void* dst, size_t bytes) {
-    if (!c) return HG_E_INVALID;
-    if (int rc = hg_ctx_flush(c)) return rc;
-    if (!c->timeline.p) return 0;
-    if (int rc = set_device(c)) return rc;
-    HG_HIP(c, hipDeviceSynchronize());
-    HG_HIP(c, hipMemcpy(dst, c->timeline.p, std::min(bytes, c->timeline.bytes), hipMemcpyDeviceToHost));
-    return int64_t(c->timeline_launches);
-}
-
 int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
     if (!c) return HG_E_INVALID;
     if (int rc = hg_ctx_flush(c)) return rc;
+    if (c->sv.running) {  // every option changes what the server's waves were launched with
+        if (int rc = set_device(c)) return rc;
+        if (int rc = server_stop(c)) return rc;
+    }
     switch (option) {
         case HG_OPT_KERNEL:
-            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_WAVEFRONT && value != HG_KERNEL_MEGA_REGEN &&
-                value != HG_KERNEL_MEGA_STREAM && value != HG_KERNEL_MEGA_POOL && value != HG_KERNEL_AUTO)
+            if (value == HG_KERNEL_WAVEFRONT || value == HG_KERNEL_MEGA_POOL)
+                return fail(c, HG_E_UNSUPPORTED, "kernel variant %d was measured, rejected and removed (DESIGN.md section 10)",
+                            value);
+            if (value != HG_KERNEL_MEGA && value != HG_KERNEL_MEGA_REGEN && value != HG_KERNEL_MEGA_STREAM &&
+                value != HG_KERNEL_AUTO)
                 return fail(c, HG_E_INVALID, "unknown kernel variant %d", value);
-            if (!HG_WITH_VARIANTS && (value == HG_KERNEL_WAVEFRONT || value == HG_KERNEL_MEGA_POOL))
-                return fail(c, HG_E_UNSUPPORTED, "kernel variant %d not built (A/B variants: make VARIANTS=1)", value);
             c->kernel = value;
             return HG_OK;
         case HG_OPT_BLOCK:
@@ -1682,10 +1689,8 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_TIMING:
             c->timing = value ? 1 : 0;
             return HG_OK;
-        case HG_OPT_REFILL:
-            if (value < 1 || value > 64) return fail(c, HG_E_INVALID, "refill must be 1..64");
-            c->refill = value;
-            return HG_OK;
+        case HG_OPT_REFILL:  // the wavefront pipeline's dequeue threshold
+            return fail(c, HG_E_UNSUPPORTED, "HG_OPT_REFILL: the wavefront pipeline was removed (DESIGN.md section 10)");
         case HG_OPT_DESCENT_T:
             if (value < -1 || value > 64) return fail(c, HG_E_INVALID, "descent threshold must be -1 (auto)..64");
             c->descent_t = value;
@@ -1715,6 +1720,9 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             return HG_OK;
         case HG_OPT_LANE_PICK:
             c->lane_pick = value ? 1 : 0;
+            return HG_OK;
+        case HG_OPT_SERVER:
+            c->server_on = value ? 1 : 0;
             return HG_OK;
         case HG_OPT_WAVE_UNITS:
             if (value < 0 || value > HG_WAVE_UNITS_LIMIT)

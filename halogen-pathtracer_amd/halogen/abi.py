@@ -84,7 +84,9 @@ class HgCounters(C.Structure):
                 ("shade_detail", C.c_uint64 * 4), ("shade_rounds", C.c_uint64), ("primary_misses", C.c_uint64),
                 ("exec_fallbacks", C.c_uint64), ("trace_busy_ms", C.c_double), ("order_faults", C.c_uint64),
                 ("scene_uploads", C.c_uint64), ("scene_uploads_skipped", C.c_uint64),
-                ("scene_uploads_partial", C.c_uint64)]
+                ("scene_uploads_partial", C.c_uint64), ("scene_uploads_vouched", C.c_uint64),
+                ("server_launches", C.c_uint64),
+                ("server_frames", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)
@@ -102,6 +104,7 @@ HG_OPT_READBACK_DEPTH = 10
 HG_OPT_READBACK_STREAM = 11
 HG_OPT_WAVE_UNITS = 12
 HG_OPT_LANE_PICK = 14
+HG_OPT_SERVER = 15
 HG_READBACK_MAX = 16
 # display formats of readback_begin(format=...) (include/halogen_abi.h, csrc/hg_pack.h): bytes per pixel and numpy view
 HG_DISPLAY_RGBA32F, HG_DISPLAY_RGBA16F, HG_DISPLAY_R11G11B10F = 0, 1, 2
@@ -110,7 +113,8 @@ DISPLAY_BPP = {HG_DISPLAY_RGBA32F: 16, HG_DISPLAY_RGBA16F: 8, HG_DISPLAY_R11G11B
 
 # every symbol include/halogen_abi.h declares (test_abi.py checks the .so exports exactly these)
 EXPORTS = [
-    "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_cubemap",
+    "hg_abi_version", "hg_create", "hg_destroy", "hg_last_error", "hg_upload_scene", "hg_upload_scene_gen",
+    "hg_upload_cubemap",
     "hg_set_params", "hg_resize", "hg_set_tiling", "hg_clear_accumulation", "hg_render", "hg_synchronize",
     "hg_readback", "hg_readback_begin", "hg_readback_end", "hg_readback_begin_format", "hg_readback_end_data",
     "hg_pack_display", "hg_set_accumulation", "hg_copy_tiles_device", "hg_local_tile_count", "hg_get_counters", "hg_reset_counters",
@@ -145,6 +149,7 @@ def lib() -> C.CDLL:
         "hg_destroy": (None, [P]),
         "hg_last_error": (C.c_char_p, [P]),
         "hg_upload_scene": (C.c_int, [P, P, i32, P, i32, P, i32, P, i32, P, i32]),
+        "hg_upload_scene_gen": (C.c_int, [P, C.c_uint64, P, i32, P, i32, P, i32, P, i32, P, i32]),
         "hg_upload_cubemap": (C.c_int, [P, i32, i32, P, sz]),
         "hg_set_params": (C.c_int, [P, C.POINTER(HgParams)]),
         "hg_resize": (C.c_int, [P, i32, i32]),
@@ -264,12 +269,13 @@ class Context:
         self.close()
 
     # --- API -----------------------------------------------------------------------------------------
-    def upload_scene(self, packed) -> None:
-        """packed: halogen.scene.PackedScene (ctypes arrays of the reference structs)."""
-        self._check(lib().hg_upload_scene(
-            self._h, _ptr(packed.spheres), len(packed.spheres), _ptr(packed.meshes), len(packed.meshes),
+    def upload_scene(self, packed, generation: int = 0) -> None:
+        """packed: halogen.scene.PackedScene (ctypes arrays of the reference structs).  generation: the caller's
+        geometry generation (hg_upload_scene_gen; 0 = compare every array)."""
+        self._check(lib().hg_upload_scene_gen(
+            self._h, int(generation), _ptr(packed.spheres), len(packed.spheres), _ptr(packed.meshes), len(packed.meshes),
             _ptr(packed.materials), len(packed.materials), _ptr(packed.triangles), len(packed.triangles),
-            _ptr(packed.blas), len(packed.blas)), "hg_upload_scene")
+            _ptr(packed.blas), len(packed.blas)), "hg_upload_scene_gen")
 
     def upload_cubemap(self, face_size: int, n_mips: int, texels: np.ndarray) -> None:
         t = np.ascontiguousarray(texels, dtype=np.float32)

@@ -153,11 +153,17 @@ class HalogenRenderPass:
         self._prior_resolution = None
         self._scene_counts = (0, 0)
         self._cubemap_uploaded = False
+        # hg_upload_scene_gen's geometry generation: bumped whenever the scene's meshes (identity, triangle and node
+        # counts, in order) differ from the last upload's, so a camera move's re-upload compares only the small arrays
+        self._geometry = (None, 0)
         self.rank, self.n_ranks = 0, 1
         # display (RP:343-347): the reference's camera target is R11G11B10 float (URP-HighFidelity.asset:26-27)
         self.display_format = abi.HG_DISPLAY_R11G11B10F
-        self.display_latency = 1  # frames the shown image lags the traced one (the C# / C++ passes' default)
+        # frames the shown image lags the traced one: 0, the reference's (it shows the frame it just traced, RP:343-345);
+        # set_display(latency=k) opts into showing k frames behind while later frames trace (the C# / C++ passes alike)
+        self.display_latency = 0
         self._display_pending = 0
+        self._display_resync = False
 
     # ---- RP:237-268 ----------------------------------------------------------------------------
     def OnCameraSetup(self, width: int, height: int):
@@ -172,6 +178,9 @@ class HalogenRenderPass:
         self.FrameCount = 1
         self.AccumulationBufferDirty = True
         self.ObjectBuffersDirty = True
+        # an image from before the clear is never shown: the readbacks in flight are ended unseen, and the next frame
+        # is shown as soon as it is traced (the pipeline refills behind it)
+        self._drop_display()
 
     def set_tiling(self, rank: int, n_ranks: int):
         """Multi-GPU: render only the 8x8 tiles t with t % n_ranks == rank (not in the reference)."""
@@ -182,7 +191,13 @@ class HalogenRenderPass:
 
     def UpdateObjectBuffers(self, scene):
         packed = scene.pack() if hasattr(scene, "pack") else scene
-        self.ctx.upload_scene(packed)
+        generation = 0  # a bare PackedScene: every array compared
+        if hasattr(scene, "meshes") and hasattr(scene, "pack"):
+            sig = tuple((id(m), m.triangle_count, len(m.bvh)) for m in scene.meshes)
+            if sig != self._geometry[0]:
+                self._geometry = (sig, self._geometry[1] + 1)
+            generation = self._geometry[1]
+        self.ctx.upload_scene(packed, generation)
         self._scene_counts = (len(packed.spheres), len(packed.meshes))
         cube = self.settings.environmentCubemap
         if self.s["UseEnvironmentCubemap"] and not self._cubemap_uploaded:
@@ -218,8 +233,9 @@ class HalogenRenderPass:
             self.FrameCount += n_frames
 
     # ---- the per-frame display (RP:343-347), pipelined, as the C# and C++ passes do it ---------------------------------
-    def set_display(self, fmt: int = abi.HG_DISPLAY_R11G11B10F, latency: int = 1):
-        """Display format (abi.HG_DISPLAY_*) and how many frames the shown image may lag (0..7)."""
+    def set_display(self, fmt: int = abi.HG_DISPLAY_R11G11B10F, latency: int = 0):
+        """Display format (abi.HG_DISPLAY_*) and how many frames the shown image may lag (0 .. HG_READBACK_MAX - 1 =
+        15; 0, the default, shows each frame before the next is traced, as the reference does)."""
         if not 0 <= latency < abi.HG_READBACK_MAX:
             raise ValueError("display latency out of range")
         self.flush_display()
@@ -231,11 +247,19 @@ class HalogenRenderPass:
         (None while the pipeline fills): (h, w) uint32 R11G11B10F, (h, w, 4) float16 or float32."""
         self.ctx.readback_begin(self.display_format)
         self._display_pending += 1
+        if self._display_resync:  # the first frame after a clear: shown at once
+            self._display_resync = False
+            return self.flush_display()
         if self._display_pending <= self.display_latency:
             return None
         self._display_pending -= 1
         w, h = self._prior_resolution
         return self.ctx.readback_end(w, h)
+
+    def _drop_display(self):
+        if self._display_pending:
+            self.flush_display()  # (ended, not shown)
+        self._display_resync = self.display_latency > 0
 
     def flush_display(self):
         """The newest display image once the readbacks in flight are done (None when none is)."""

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 4
+#define HG_ABI_VERSION 5
 
 /* ----------------------------------------------------------------------------------------------
  * Reference host structs (byte-identical to the C# [Sequential] structs)
@@ -176,6 +176,10 @@ typedef struct hg_counters {
     uint64_t scene_uploads_partial; /* ... of scene_uploads, those whose triangles and BVH entries equalled the last
                                        upload's (objects moved, materials changed): only the mesh table, spheres and
                                        materials were rebuilt */
+    uint64_t scene_uploads_vouched; /* ... of the skipped and partial ones, those whose triangles and BVH entries were
+                                       vouched for by an unchanged geometry generation (hg_upload_scene_gen), not compared */
+    uint64_t server_launches;       /* render server lifetimes started (HG_OPT_SERVER), since hg_create */
+    uint64_t server_frames;         /* frames posted to a render server, since hg_create */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -196,21 +200,18 @@ enum {
  *   ends starts its next sample / frame at once (per-lane path regeneration), so no lane idles until the
  *   longest path of its wave ends.  Falls back to MEGA when maxBounces > 250 or samplesPerPixel >= 65535.
  * MEGA: the lockstep form — each lane traces whole paths, frame after frame (also runs the debug views 1-5).
- * WAVEFRONT: gen/trace/shade kernels over compacted ray queues (A/B alternative; slower on this workload, the
- *   queue round trips cost more than the lane utilisation they recover). */
-/* MEGA_STREAM: MEGA_REGEN with a resumable traversal — lanes that finished traversing shade and start their next
- *   ray while the stragglers keep traversing (same limits and fallback as MEGA_REGEN). */
-/* MEGA_POOL: each wave owns several tiles' paths (more paths than lanes) in a slot array and alternates a trace
- *   phase (lanes refill from a queue of ready rays as their traversal finishes) with a shade phase (same limits and
- *   fallback as MEGA_REGEN). */
-/* AUTO (default): MEGA_STREAM when the scene has a BLAS deeper than 16 levels, else MEGA_REGEN. */
+ * MEGA_STREAM: MEGA_REGEN with a resumable traversal — lanes that finished traversing shade and start their next
+ *   ray while the stragglers keep traversing (same limits and fallback as MEGA_REGEN).
+ * AUTO (default): MEGA_STREAM when the scene has a BLAS deeper than 16 levels or at least 4 meshes, else MEGA_REGEN.
+ * WAVEFRONT and MEGA_POOL (gen/trace/shade kernels over compacted ray queues; several tiles' paths per wave) were
+ *   measured slower, rejected, and removed in round 5: selecting them returns HG_E_UNSUPPORTED. */
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
        HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5 };
 /* HG_OPT_BLOCK: workgroup size of the lockstep kernel HG_KERNEL_MEGA (64/128/256; the debug views, large-maxBounces
  *   fallback) and of the wavefront trace kernel; the regenerating / streaming / pool kernels always run one-wave
  *   workgroups (their per-lane LDS rows assume it) and ignore it.  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
- * HG_OPT_REFILL: traversal lanes idle before a wave dequeues new rays (1..64).
+ * HG_OPT_REFILL: (the removed wavefront pipeline's dequeue threshold) returns HG_E_UNSUPPORTED.
  * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then
  *   blended in frame order, bit-identical): 0 = automatic (about 6 launches' worth of the GPU's wave slots per
  *   launch — keeps small images and one rank's 1/N share at N GPUs filling the GPU), 1 = never, k = k per tile.
@@ -230,7 +231,15 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
        HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
-       HG_OPT_LANE_PICK = 14 };
+       HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15 };
+/* HG_OPT_SERVER (default 1): hg_render calls of at most 8 accumulating frames on the streaming kernel (the reference's
+ *   one dispatch per frame, RP:327) post their frames to a render server — persistent trace waves that outlive the call
+ *   and take each posted frame's (tile, frame) units as soon as lanes free up, so one frame's last paths overlap the
+ *   next frame's first — instead of launching.  Each frame's blend runs on the context stream behind a gate on that
+ *   frame's completion, in frame order, so every readback / gather sees exactly the frames rendered before it.  The
+ *   server is stopped (its waves trace what was posted, then leave) by uploads, resize, tiling, options, counters,
+ *   hg_synchronize, hg_destroy, a launch of another kind, or parameters / FrameCount that do not continue its chain.
+ *   0 = every call launches (the round-4 per-launch pipeline).  Same images either way. */
 /* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
  *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
  *   device image and copied on the context stream.  Same images either way. */
@@ -259,6 +268,18 @@ int hg_upload_scene(hg_ctx* ctx,
                     const PackedHalogenMaterial* materials, int32_t n_materials,
                     const HalogenTriangle* triangles, int32_t n_triangles,
                     const BVHEntry* blas, int32_t n_nodes);
+/* hg_upload_scene with the caller's geometry generation: a non-zero generation equal to the last successful upload's
+ * vouches that the triangles and BVH entries are that upload's (the caller bumps it whenever its mesh registry —
+ * RayTracingManager's mesh list in the reference — changes), so they are not compared; the spheres, mesh records and
+ * materials are compared as always (the reference re-reads transforms and materials on every re-upload, RP:448-509).
+ * The reference re-uploads every buffer on each camera move (RP:262-268, 296-299): this keeps that call pattern at the
+ * cost of the small arrays only.  Generation 0 (and every generation change) compares everything, as hg_upload_scene. */
+int hg_upload_scene_gen(hg_ctx* ctx, uint64_t geometry_generation,
+                        const HalogenSphere* spheres, int32_t n_spheres,
+                        const HalogenMeshData* meshes, int32_t n_meshes,
+                        const PackedHalogenMaterial* materials, int32_t n_materials,
+                        const HalogenTriangle* triangles, int32_t n_triangles,
+                        const BVHEntry* blas, int32_t n_nodes);
 
 /* Environment cubemap (EnvironmentCubemap, HalgoenCompute.compute:48): RGBA32F texels, layout
  * [mip][face][y][x][4], faces +X,-X,+Y,-Y,+Z,-Z, mip m is max(1, face_size >> m) square.

@@ -168,6 +168,10 @@ struct SceneBuffers {
     std::vector<PackedHalogenMaterial> materials;
     std::vector<HalogenTriangle> triangles;
     std::vector<BVHEntry> blas;
+    // The producer's geometry generation (hg_upload_scene_gen): bump it whenever `triangles` / `blas` change; while it
+    // stays the same (non-zero), a re-upload (every camera move, RP:262-268) compares only the small arrays.  0: compare
+    // everything.
+    uint64_t geometry_generation = 0;
 };
 
 class HalogenRenderPass {
@@ -192,11 +196,14 @@ class HalogenRenderPass {
         prior_h_ = height;
     }
 
-    // RP:262-268
+    // RP:262-268.  An image from before the clear is never shown: the display readbacks in flight are ended unseen, and
+    // the next frame is shown as soon as it is traced (the pipeline refills behind it).
     void ClearAccumulation() {
         FrameCount = 1;
         AccumulationBufferDirty = true;
         ObjectBuffersDirty = true;
+        if (display_pending_ > 0) (void)FlushDisplay();
+        display_resync_ = display_latency_ > 0;
     }
 
     // Multi-GPU (not in the reference): this pass renders only the 8x8 tiles t with t % n_ranks == rank
@@ -208,11 +215,11 @@ class HalogenRenderPass {
 
     // RP:448-509 (the buffers are copied, SetBufferData semantics)
     void UpdateObjectBuffers(const SceneBuffers& sc) {
-        check(hg_upload_scene(ctx_, sc.spheres.data(), int32_t(sc.spheres.size()), sc.meshes.data(),
-                              int32_t(sc.meshes.size()), sc.materials.data(), int32_t(sc.materials.size()),
-                              sc.triangles.data(), int32_t(sc.triangles.size()), sc.blas.data(),
-                              int32_t(sc.blas.size())),
-              "hg_upload_scene");
+        check(hg_upload_scene_gen(ctx_, sc.geometry_generation, sc.spheres.data(), int32_t(sc.spheres.size()),
+                                  sc.meshes.data(), int32_t(sc.meshes.size()), sc.materials.data(),
+                                  int32_t(sc.materials.size()), sc.triangles.data(), int32_t(sc.triangles.size()),
+                                  sc.blas.data(), int32_t(sc.blas.size())),
+              "hg_upload_scene_gen");
         n_spheres_ = int32_t(sc.spheres.size());
         n_meshes_ = int32_t(sc.meshes.size());
         if (s_.UseEnvironmentCubemap && !cubemap_uploaded_) {
@@ -251,7 +258,8 @@ class HalogenRenderPass {
     // The reference's per-frame display (RP:343-347: the accumulation target blitted into the URP camera colour target,
     // an R11G11B10 HDR target under URP-HighFidelity.asset:26-27) as a host image, pipelined: Display() enqueues the
     // display readback of every frame rendered so far in the display format and returns the image of `latency` calls
-    // ago (an empty image while the pipeline fills), so the next Execute traces while that image crosses PCIe.
+    // ago (an empty image while the pipeline fills), so the next Execute traces while that image crosses PCIe.  The
+    // default latency is 0: each frame's image before the next is traced, as the reference shows it (RP:343-345).
     // FlushDisplay() waits for the readbacks in flight and returns the newest image.  The pointer stays valid until
     // the next Display / FlushDisplay / OnCameraSetup with a new size.
     struct DisplayImage {
@@ -271,6 +279,10 @@ class HalogenRenderPass {
     DisplayImage Display() {
         check(hg_readback_begin_format(ctx_, display_format_), "hg_readback_begin_format");
         ++display_pending_;
+        if (display_resync_) {  // the first frame after a clear: shown at once
+            display_resync_ = false;
+            return FlushDisplay();
+        }
         if (display_pending_ <= display_latency_) return DisplayImage{};
         return end_display();
     }
@@ -338,7 +350,8 @@ class HalogenRenderPass {
     HalogenSettings settings_;
     ClampedSettings s_;
     hg_ctx* ctx_ = nullptr;
-    int32_t display_format_ = HG_DISPLAY_R11G11B10F, display_latency_ = 1, display_pending_ = 0;
+    int32_t display_format_ = HG_DISPLAY_R11G11B10F, display_latency_ = 0, display_pending_ = 0;
+    bool display_resync_ = false;
     int32_t prior_w_ = -1, prior_h_ = -1;
     hg_vec3 prior_position_{};  // PriorCameraPosition / PriorCameraRotation (RP:293-294)
     hg_vec4 prior_rotation_{};

@@ -12,6 +12,7 @@ from halogen import scenes
 # name: (config, width, height, frames, accumulate, overrides)
 CASES = {
     "c1_64": ("C1", 64, 64, 4, True, {}),
+    "c1_256": ("C1", 256, 256, 1, True, {}),  # BASELINE.json configs[0]: the Cornell box at 256x256, 1 spp
     "c1_64_spp3": ("C1", 64, 64, 1, True, {"SamplesPerPixel": 3}),
     "c1_48_noacc": ("C1", 48, 48, 2, False, {"Accumulate": False}),
     "c1_40x24_bounce12": ("C1", 40, 24, 3, True, {"MaxBounces": 12, "DiffuseBounces": 12}),

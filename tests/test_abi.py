@@ -63,7 +63,7 @@ def test_library_exports_every_declared_symbol(built):
     missing = [s for s in declared if s not in exported]
     assert not missing, missing
     L = abi.lib()  # loads, binds every signature
-    assert L.hg_abi_version() == 4
+    assert L.hg_abi_version() == 5
 
 
 def test_no_gpu_is_a_loud_error(built):

@@ -35,7 +35,7 @@ def test_native_calls_are_declared_and_exported():
     called = set(re.findall(r"HalogenNative\.(hg_\w+)\(", PASS))
     declared = set(re.findall(r"extern \w+ (hg_\w+)\(", NATIVE))
     exported = set(re.findall(r"^\w[\w\s\*]*?\b(hg_\w+)\(", HEADER, re.M))
-    assert {"hg_create", "hg_upload_scene", "hg_set_params", "hg_render", "hg_readback_begin_format",
+    assert {"hg_create", "hg_upload_scene_gen", "hg_set_params", "hg_render", "hg_readback_begin_format",
             "hg_readback_end_data", "hg_set_accumulation", "hg_destroy",
             "hg_comm_init_all", "hg_comm_gather", "hg_comm_readback_begin", "hg_comm_readback_end"} <= called
     assert called <= declared <= exported, (called - declared, declared - exported)

@@ -86,31 +86,47 @@ def test_gpu_display_format_tiling(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_render_pass_display_one_frame_behind(gpu):
-    """The Python HalogenRenderPass's display (as the C# and C++ passes): one Execute per frame, each display() returns
-    the previous frame's R11G11B10F image; a moving camera restarts the accumulation and the display follows."""
+def test_gpu_render_pass_display_latency_and_clear(gpu):
+    """The Python HalogenRenderPass's display (as the C# and C++ passes): by default (latency 0, the reference's) each
+    display() returns the frame just traced; with latency 1, the previous frame's image.  A camera move
+    (ClearAccumulation, RP:262-268) ends the readbacks in flight unseen and shows the first moved frame at once, so no
+    image from before the clear is ever shown."""
     from halogen import render_pass as rp, scenes
+    from halogen.unity import Transform
     cfg = scenes.CONFIGS["C1"].resized(40, 32, 4)
     scene = cfg.build_scene()
     cam = cfg.camera()
+    t = cam.transform
+    moved = rp.Camera(Transform((t.position[0] + 0.05, t.position[1], t.position[2]), tuple(t.rotation)),
+                      cam.fieldOfView, cam.pixelWidth, cam.pixelHeight)
+    views = [cam] * 4 + [moved] * 3
     ref = rp.HalogenRenderPass(cfg.settings)
     want = []
-    for _ in range(4):
-        ref.Execute(scene, cam)
+    for c in views:
+        ref.Execute(scene, c)
         want.append(abi.pack_display(ref.read_image(), abi.HG_DISPLAY_R11G11B10F))
     ref.Dispose()
     p = rp.HalogenRenderPass(cfg.settings)
+    assert p.display_latency == 0
+    for k in range(2):
+        p.Execute(scene, views[k])
+        assert np.array_equal(p.display(), want[k]), k
+    p.Dispose()
+    p = rp.HalogenRenderPass(cfg.settings)
+    p.set_display(abi.HG_DISPLAY_R11G11B10F, 1)
     got = []
-    for _ in range(4):
-        p.Execute(scene, cam)
+    for c in views:
+        p.Execute(scene, c)
         got.append(p.display())
     assert got[0] is None  # the pipeline fills
-    last = p.flush_display()
-    for k in range(1, 4):
+    for k in (1, 2, 3):
         assert np.array_equal(got[k], want[k - 1]), k
-    assert np.array_equal(last, want[3])
+    assert np.array_equal(got[4], want[4]), "the first frame after the camera move, shown at once"
+    assert got[5] is None  # the pipeline refills behind it
+    assert np.array_equal(got[6], want[5])
+    assert np.array_equal(p.flush_display(), want[6])
     p.set_display(abi.HG_DISPLAY_RGBA16F, 0)  # at once
-    p.Execute(scene, cam)
+    p.Execute(scene, moved)
     img = p.display()
     assert img.dtype == np.float16 and np.array_equal(img.view(np.uint16),
                                                        abi.pack_display(p.read_image(), abi.HG_DISPLAY_RGBA16F).view(np.uint16))

@@ -18,8 +18,6 @@ REL_TOL = 1e-4  # north_star: "within 1e-4 relative fp32"; asserted only as a di
 
 KERNELS = {"mega": abi.HG_KERNEL_MEGA, "regen": abi.HG_KERNEL_MEGA_REGEN, "stream": abi.HG_KERNEL_MEGA_STREAM,
            "auto": abi.HG_KERNEL_AUTO}
-if os.environ.get("HG_TEST_VARIANTS") == "1":  # library built with make VARIANTS=1 (the A/B kernels)
-    KERNELS.update({"wavefront": abi.HG_KERNEL_WAVEFRONT, "pool": abi.HG_KERNEL_MEGA_POOL})
 
 
 def gpu_render(packed, params, frames, acc=True, cube=None, tiling=None, ctx=None, splits=None, kernel="auto",

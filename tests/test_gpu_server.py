@@ -1,0 +1,226 @@
+"""The render server (HG_OPT_SERVER, csrc/hg_mega.hip kServer), through the C-ABI.
+
+The reference dispatches HalogenCompute once per frame (RP:327, RP:406).  hg_render calls of few accumulating frames on
+the streaming kernel post their frames to persistent trace waves that outlive the call; each frame's blend runs on the
+context stream behind a gate on that frame's completion count.  Every image here is compared bit for bit with the
+batched launch (or the committed golden and its counters), with the server off (every call its own launch), and across
+every event that stops or restarts the server: a new camera, a checkpoint, a clear, counters, an idle gap, a launch of
+another kind, readbacks in flight."""
+import json
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import cases
+from halogen import abi, render_pass as rp, scenes
+from test_gpu_parity import assert_bitwise, gpu_render
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _ctx(packed, params, cube=None, server=1, coalesce=1, tiling=None):
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    ctx = abi.Context(0)
+    ctx.set_option(abi.HG_OPT_SERVER, server)
+    ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
+    ctx.upload_scene(packed)
+    if cube is not None:
+        ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+    ctx.resize(W, H)
+    if tiling:
+        ctx.set_tiling(*tiling)
+    ctx.set_params(params)
+    return ctx, W, H
+
+
+def _sized(cfg_name, w, h, frames=1):
+    cfg = scenes.CONFIGS[cfg_name].resized(w, h, frames)
+    settings = scenes.settings_for(cfg)
+    packed = cases._scene(cfg.scene, 10)
+    s = rp.clamp_settings(settings)
+    cube = settings.environmentCubemap if s["UseEnvironmentCubemap"] else None
+    return packed, rp.make_params(s, cfg.camera(), 1, len(packed.spheres), len(packed.meshes), cube is not None), cube
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dragon10_64x36", "c1_64", "c1_64_spp3"])
+def test_gpu_server_one_frame_calls_match_golden(gpu, name):
+    """frames x hg_render(1) through one server lifetime: the golden image and its counters (the server's waves count
+    every ray, triangle and box test as the per-launch kernels do), one server launch, every frame posted."""
+    meta = json.loads((GOLD / f"{name}.json").read_text())
+    packed, params, cube, frames, acc = cases.setup(name)
+    ctx, W, H = _ctx(packed, params, cube)
+    with ctx:
+        for _ in range(frames):
+            ctx.render(1, True)
+        img = ctx.readback(W, H)
+        cnt = ctx.counters()
+    assert_bitwise(img, np.load(GOLD / f"{name}.npz")["image"], f"{name}: {frames} frames through the server")
+    for k, v in meta["counters"].items():
+        assert cnt[k] == v, (k, cnt[k], v)
+    assert cnt["server_launches"] == 1 and cnt["server_frames"] == frames, cnt
+
+
+@pytest.mark.gpu
+def test_gpu_server_off_launches_per_call(gpu):
+    """HG_OPT_SERVER 0: every call its own launch (the round-4 pipeline), the same image; no server launched."""
+    packed, params, cube, frames, acc = cases.setup("dragon10_64x36")
+    ref, _ = gpu_render(packed, params, frames, True, cube)
+    ctx, W, H = _ctx(packed, params, cube, server=0)
+    with ctx:
+        for _ in range(frames):
+            ctx.render(1, True)
+        img = ctx.readback(W, H)
+        cnt = ctx.counters()
+    assert_bitwise(img, ref, "server off")
+    assert cnt["server_launches"] == 0 and cnt["launches"] == frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frames", [3, 40, 200])
+def test_gpu_server_many_frames_match_batched(gpu, frames):
+    """More frames than the colour ring (16) and the per-wave frame window (4) hold, posted one per call, in pairs and
+    in eights (hg_render(n <= 8) posts n frames), as one rank's share of a 3-way tiling too: the batched image."""
+    packed, params, cube, _, _ = cases.setup("dragon10_64x36")
+    for tiling in (None, (2, 3)):
+        ref, rc = gpu_render(packed, params, frames, True, cube, tiling=tiling)
+        for per_call in (1, 2, 8):
+            ctx, W, H = _ctx(packed, params, cube, tiling=tiling)
+            with ctx:
+                done = 0
+                while done < frames:
+                    n = min(per_call, frames - done)
+                    ctx.render(n, True)
+                    done += n
+                img = np.full((H, W, 4), np.nan, np.float32)
+                ctx.readback(W, H, img)
+                cnt = ctx.counters()
+            assert_bitwise(img, ref, f"{frames} frames, {per_call} per call, tiling {tiling}")
+            assert cnt["server_frames"] == frames and cnt["paths"] == rc["paths"], cnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [1, 2, 4])
+def test_gpu_server_display_readback(gpu, depth):
+    """The C# pass's per-frame display: render(1), readback_begin, and readback_end once `depth` are outstanding (0, 1
+    and 3 frames behind).  Each displayed image (R11G11B10F and RGBA32F) equals that many frames' image; the server
+    serves every frame of the run (one launch)."""
+    packed, params, cube, _, _ = cases.setup("dragon10_64x36")
+    n = 12
+    want = [gpu_render(packed, params, k, True, cube)[0] for k in range(1, n + 1)]
+    for fmt in (abi.HG_DISPLAY_RGBA32F, abi.HG_DISPLAY_R11G11B10F):
+        ctx, W, H = _ctx(packed, params, cube)
+        with ctx:
+            ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+            got, pending = [], 0
+            for _ in range(n):
+                ctx.render(1, True)
+                ctx.readback_begin(fmt)
+                pending += 1
+                if pending == depth:
+                    got.append(ctx.readback_end(W, H))
+                    pending -= 1
+            while pending:
+                got.append(ctx.readback_end(W, H))
+                pending -= 1
+            cnt = ctx.counters()
+        for k, img in enumerate(got):
+            exp = want[k] if fmt == abi.HG_DISPLAY_RGBA32F else abi.pack_display(want[k], fmt)
+            assert np.array_equal(np.asarray(img).view(np.uint8), np.asarray(exp).view(np.uint8)), \
+                f"display depth {depth}, format {fmt}, frame {k + 1}"
+        assert cnt["server_launches"] == 1 and cnt["server_frames"] == n, cnt
+
+
+@pytest.mark.gpu
+def test_gpu_server_restarts_keep_the_image(gpu):
+    """Every event that ends a server lifetime, mid-run, against the same call sequence with the server off: a camera
+    move (set_params with a new camera and FrameCount 1, then clear, as ClearAccumulation does, RP:262-268), a
+    checkpoint (set_accumulation), a clear alone (the server keeps running: the clear is ordered between blends), a
+    counters read, a launch of another kind (a 16-frame call), an idle gap longer than the server's, an upload."""
+    packed, params, cube, _, _ = cases.setup("dragon10_64x36")
+    moved = cases.setup("dragon10_64x36")[1]
+    moved.camLocalToWorld.m[12] += 0.05
+
+    def run(server):
+        ctx, W, H = _ctx(packed, params, cube, server=server)
+        imgs = []
+        with ctx:
+            def frames(k):
+                for _ in range(k):
+                    ctx.render(1, True)
+                imgs.append(ctx.readback(W, H))
+            frames(5)
+            ctx.set_params(moved)
+            ctx.clear_accumulation()
+            frames(4)
+            ctx.set_accumulation(imgs[0], 6)
+            frames(3)
+            ctx.clear_accumulation()
+            frames(3)
+            ctx.counters()
+            frames(2)
+            ctx.render(16, True)
+            frames(2)
+            time.sleep(0.08)
+            frames(2)
+            ctx.upload_scene(packed)
+            frames(2)
+            cnt = ctx.counters()
+        return imgs, cnt
+
+    on, con = run(1)
+    off, coff = run(0)
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert_bitwise(a, b, f"server restarts, readback {k}")
+    assert con["server_launches"] >= 6 and coff["server_launches"] == 0, (con, coff)
+    for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+        assert con[k] == coff[k], (k, con[k], coff[k])
+
+
+@pytest.mark.gpu
+def test_gpu_server_edge_tiles_and_small_images(gpu):
+    """Images whose size is not a multiple of 8 (edge tiles of fewer than 64 pixels), a single tile (8x8: one unit per
+    frame, fewer units than the server has waves), and a power-of-two tile count (the unit -> frame shift)."""
+    for w, h in ((61, 35), (8, 8), (64, 64)):
+        packed, params, cube = _sized("C3", w, h)
+        ref, _ = gpu_render(packed, params, 24, True, cube)
+        ctx, W, H = _ctx(packed, params, cube)
+        with ctx:
+            for _ in range(24):
+                ctx.render(1, True)
+            img = ctx.readback(W, H)
+            cnt = ctx.counters()
+        assert_bitwise(img, ref, f"{w}x{h} through the server")
+        assert cnt["server_launches"] == 1, cnt
+
+
+@pytest.mark.gpu
+def test_gpu_server_full_size_c3_with_display(gpu):
+    """BASELINE's C3 at 1920x1080: 64 x (render(1) + R11G11B10F display one frame behind) through one server lifetime
+    is bit-identical to hg_render(64), and every displayed image is the host packing of that frame's fp32 image (checked
+    for the last two, the rest against the batched images of a few frame counts)."""
+    cfg = scenes.CONFIGS["C3"]
+    packed, params, cube = _sized("C3", cfg.width, cfg.height)
+    W, H = cfg.width, cfg.height
+    checks = {1, 2, 17, 63, 64}
+    want = {k: gpu_render(packed, params, k, True, cube)[0] for k in checks}
+    ctx, _, _ = _ctx(packed, params, cube)
+    with ctx:
+        ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 2)
+        shown, pending = [], 0
+        for _ in range(64):
+            ctx.render(1, True)
+            ctx.readback_begin(abi.HG_DISPLAY_R11G11B10F)
+            pending += 1
+            if pending == 2:
+                shown.append(ctx.readback_end(W, H))
+                pending -= 1
+        shown.append(ctx.readback_end(W, H))
+        img = ctx.readback(W, H)
+        cnt = ctx.counters()
+    assert_bitwise(img, want[64], "C3 1080p, 64 frames through the server")
+    for k in checks:
+        assert np.array_equal(shown[k - 1], abi.pack_display(want[k], abi.HG_DISPLAY_R11G11B10F)), f"displayed frame {k}"
+    assert cnt["server_launches"] == 1 and cnt["server_frames"] == 64, cnt
