@@ -375,6 +375,59 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
             "scene_uploads_total": c["scene_uploads"], "host_threads_upload": 16}
 
 
+def strong_scaling_measurement(ctx, params, W, H, fps: int, steps: int, world: int, rank: int, emu: int, barrier,
+                               gather_fn, coll_dev, dist, ref_img=None) -> dict:
+    """The strong-scaling leg, beside the weak line: the FIXED image of `fps` frames per step (C3: 64),
+    its 8x8 tiles dealt round-robin to the N ranks (HC:1033: pixels are independent), so the ranks share one image's work
+    instead of each doing one image's worth.  Same clock as the headline (barrier + device sync on both sides, max over
+    ranks) around `steps` x hg_render(fps) and the gather of the tiles to rank 0.  Reports the value, the ms per step, and
+    each rank's tile count and trace time (its renders' completion on its own clock, before the gather), so load balance
+    shows.  N > 1: rank 0 compares the gathered image with `ref_img` (the same frames on one context, all tiles) bit for
+    bit.  --emulate-ranks N (one GPU): rank 0's share alone, and the rate N such shares would reach if equally fast."""
+    ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.render(fps, True)  # warm-up (this share's cost order)
+    ctx.clear_accumulation()
+    ctx.set_params(params)
+    ctx.reset_counters()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.render(fps, True)
+    ctx.synchronize()
+    t_trace = time.perf_counter() - t0
+    gathered = gather_fn() if world > 1 else None
+    barrier()
+    dt = time.perf_counter() - t0
+    c = ctx.counters()
+    mine = [dt, t_trace, float(ctx.local_tile_count()), c.get("trace_busy_ms", 0.0)]
+    per_rank = [mine]
+    if dist is not None:
+        import torch
+
+        t = torch.tensor(mine, dtype=torch.float64, device=coll_dev)
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        per_rank = [x.tolist() for x in out]
+    dt_max = max(r[0] for r in per_rank)
+    n = emu or world
+    paths = W * H * fps * steps if not emu else ctx.local_tile_count() * 64 * fps * steps
+    res = {"scaling": "strong", "workload": f"one {W}x{H} image of {fps} frames per step, its tiles over {n} ranks",
+           "n_ranks": n, "steps": steps, "value": paths / dt_max / 1e6, "unit": "Mpaths/s",
+           "ms_per_step": dt_max * 1e3 / steps,
+           "per_rank": [{"rank": r, "tiles": int(v[2]), "trace_ms_per_step": v[1] * 1e3 / steps,
+                         "total_ms_per_step": v[0] * 1e3 / steps, "trace_busy_ms": v[3]} for r, v in enumerate(per_rank)],
+           "trace_balance": min(v[1] for v in per_rank) / max(v[1] for v in per_rank)}
+    if emu:
+        res["emulated"] = f"rank 0's share of {n} on one GPU: value is that share's rate; x{n} if every share ran alike"
+        res["value_if_balanced"] = res["value"] * n
+    if rank == 0 and world > 1 and gathered is not None and ref_img is not None:
+        g = gathered if isinstance(gathered, np.ndarray) else gathered.cpu().numpy()
+        res["gathered_bit_identical_to_one_context"] = bool(np.array_equal(g.view(np.uint32), ref_img.view(np.uint32)))
+    return res
+
+
 def committed_counters(config: str, W: int, H: int, frames_per_launch: int, kernel_symbol: str) -> dict:
     """The committed PMC figures of this workload's production kernel (tools/summarize_profile.py):
     profiles/pmc_traffic_<config>.json, or profiles/pmc_traffic.json (the headline config's), when they match the
@@ -575,6 +628,7 @@ def main():
     ap.add_argument("--sah-leaf", type=int, default=2, help="--bvh sah: largest leaf the SAH build makes by size alone")
     ap.add_argument("--no-fast-bvh", action="store_true", help="skip the fast_bvh leg (C3 on an SAH BLAS)")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1 / --emulate-ranks: skip the strong-scaling leg")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
                          "reports that rank's own Mpaths/s, not a contract line")
@@ -875,6 +929,35 @@ def main():
     else:
         totals = cnt
 
+    strong = None
+    if (dist is not None or emu) and not args.no_strong:
+        def strong_gather():
+            if comm is not None:
+                comm.gather(0)
+                comm.synchronize()
+                return comm.readback(W, H) if rank == 0 else None
+            import torch
+
+            from halogen import distributed as hd
+
+            loc = torch.empty((ctx.local_tile_count(), 64, 4), dtype=torch.float32, device=f"cuda:{device}")
+            ctx.copy_tiles_device(loc.data_ptr(), loc.numel() * 4)
+            return hd.gather_tiles(loc.to(coll_dev), rank, world, W, H, on_device=True)
+
+        ref_img = None
+        if rank == 0 and dist is not None:  # the same frames on one context, all tiles (untimed)
+            with abi.Context(device) as one:
+                one.upload_scene(packed)
+                if cube is not None:
+                    one.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+                one.resize(W, H)
+                one.set_params(params)
+                for _ in range(args.steps):
+                    one.render(args.frames_per_step, True)
+                ref_img = one.readback(W, H)
+        strong = strong_scaling_measurement(ctx, params, W, H, args.frames_per_step, args.steps, world, rank, emu,
+                                            barrier, strong_gather, coll_dev, dist, ref_img)
+
     total_paths = W * H * frames_per_step * args.steps
     if emu:  # this GPU traced only its 1/N share of the tiles
         total_paths = ctx.local_tile_count() * 64 * frames_per_step * args.steps
@@ -931,6 +1014,8 @@ def main():
                                        (x / (cnt["trace_cycles"] + cnt["shade_cycles"]) for x in cnt["shade_detail"])))
             if counters_ok and any(cnt.get("shade_detail", [])) else None,
             "emulated_ranks": emu or None,
+            # N > 1: the same image's work split over the ranks (strong scaling), beside the weak line above
+            "strong_scaling": strong,
             # N > 1: every pixel of the gathered image was written by some rank (alpha of a blended pixel is ~1)
             "gather_complete": bool((gathered[..., 3] > 0.5).all().item()) if gathered is not None else None,
             "gather": (gather_mode + (f" (hg_comm transport {comm.transport})" if comm is not None else
