@@ -10,6 +10,8 @@
 // centre/extents, so every min/max goes through  e=(max-min)*0.5, c=min+e, min=c-e, max=c+e.
 // Compiled with -ffp-contract=off.
 #include <atomic>
+#include <cfloat>
+#include <cmath>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -556,13 +558,25 @@ struct Box3 {
 
 constexpr int kSahBins = 32;
 
+// The bin of a centroid coordinate: computed and clamped in float, so that no float -> int conversion is out of range
+// (a centroid span of a few ulps gives a scale near FLT_MAX, and (c - lo) * scale may then overflow to inf)
+inline int sah_bin(float c, float lo, float scale) {
+    const float f = (c - lo) * scale;
+    if (!(f > 0.0f)) return 0;
+    if (!(f < float(kSahBins - 1))) return kSahBins - 1;
+    return int(f);
+}
+
 }  // namespace
 
 extern "C" int64_t hg_build_blas_sah(const float* V, int32_t n_vertices, int32_t* idx, int32_t n_tris,
                                      int32_t max_leaf, int32_t max_depth, BVHEntry* out_nodes, int64_t max_nodes) {
     if (!V || !idx || n_tris < 0 || n_vertices < 0 || max_leaf < 1 || max_leaf > 15 || max_depth < 1) return HG_E_INVALID;
-    for (int64_t i = 0; i < 3 * int64_t(n_tris); ++i)
+    for (int64_t i = 0; i < 3 * int64_t(n_tris); ++i) {
         if (idx[i] < 0 || idx[i] >= n_vertices) return HG_E_INVALID;
+        const float* p = V + 3 * size_t(idx[i]);  // a NaN or infinite vertex has no box (and no bin)
+        if (!std::isfinite(p[0]) || !std::isfinite(p[1]) || !std::isfinite(p[2])) return HG_E_INVALID;
+    }
     const size_t n = size_t(n_tris);
     std::vector<Box3> tb(n);
     std::vector<float> cen(3 * n);
@@ -608,14 +622,13 @@ extern "C" int64_t hg_build_blas_sah(const float* V, int32_t n_vertices, int32_t
         double best_cost = std::numeric_limits<double>::infinity();
         for (int ax = 0; ax < 3; ++ax) {
             const float ext = cb.hi[ax] - cb.lo[ax];
-            if (!(ext > 0.0f)) continue;
+            const float scale = float(kSahBins) / ext;
+            if (!(ext > 0.0f) || !(scale < FLT_MAX)) continue;  // one centroid plane (or a span of denormals)
             Box3 bins[kSahBins];
             uint32_t cnt[kSahBins] = {};
-            const float scale = float(kSahBins) / ext;
             for (uint32_t i = first; i < first + count; ++i) {
                 const uint32_t t = ord[i];
-                int b = int((cen[3 * size_t(t) + ax] - cb.lo[ax]) * scale);
-                b = b < 0 ? 0 : b >= kSahBins ? kSahBins - 1 : b;
+                const int b = sah_bin(cen[3 * size_t(t) + ax], cb.lo[ax], scale);
                 bins[b].add(tb[t]);
                 cnt[b]++;
             }
@@ -652,8 +665,7 @@ extern "C" int64_t hg_build_blas_sah(const float* V, int32_t n_vertices, int32_t
             uint32_t* lo = ord.data() + first;
             uint32_t* hi = ord.data() + first + count;
             while (lo < hi) {
-                int b = int((cen[3 * size_t(*lo) + best_axis] - cb.lo[best_axis]) * scale);
-                b = b < 0 ? 0 : b >= kSahBins ? kSahBins - 1 : b;
+                const int b = sah_bin(cen[3 * size_t(*lo) + best_axis], cb.lo[best_axis], scale);
                 if (uint32_t(b) <= best_bin) ++lo;
                 else std::swap(*lo, *--hi);
             }

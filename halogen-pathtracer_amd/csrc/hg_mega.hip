@@ -428,6 +428,13 @@ __global__ __launch_bounds__(64) void hg_order_verify_mark(const uint32_t* __res
     if (v < n) atomicAdd(&seen[v], 1u);
     else atomicAdd(faults, 1ull);
 }
+// HG_CHECK_EXEC builds: words that every use leaves zeroed (the sort's histogram / claims / done count, a queue
+// launch's heads and exit count) must read zero when the next use starts; each that does not counts into *faults
+__global__ __launch_bounds__(64) void hg_check_zeroed(const uint32_t* __restrict__ p, uint32_t n,
+                                                      unsigned long long* __restrict__ faults) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i < n && p[i] != 0u) atomicAdd(faults, 1ull);
+}
 __global__ __launch_bounds__(64) void hg_order_verify_count(uint32_t n, uint32_t* __restrict__ seen,
                                                             unsigned long long* __restrict__ faults) {
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
@@ -447,6 +454,11 @@ hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint
     if (n == 0) return hipSuccess;
     HgOrderScratch* sc = static_cast<HgOrderScratch*>(scratch);
     const dim3 g{(n + kOrderTilesPerGroup - 1) / kOrderTilesPerGroup};
+#if HG_CHECK_EXEC
+    if (faults)
+        hipLaunchKernelGGL(hg_check_zeroed, dim3((2049u + 63u) / 64u), dim3(64), 0, stream,
+                           static_cast<const uint32_t*>(scratch), 2049u, faults);
+#endif
     hipLaunchKernelGGL(hg_order_hist, g, dim3(64), 0, stream, cost, n, sc);
     hipLaunchKernelGGL(hg_order_scatter, g, dim3(64), 0, stream, cost, order, n, sc, faults);
 #if HG_CHECK_EXEC
@@ -1428,6 +1440,11 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
     const size_t mesh_lds = mesh_lds_bytes(lds, kp.n_meshes, HG_WAVE_LDS_BUDGET);
     const dim3 g{uint32_t(grid)}, b{64u};
     const size_t sh = mesh_lds ? mesh_lds : lds;
+#if HG_CHECK_EXEC
+    if (queue && !server && kp.counters)  // the last wave of the previous launch zeroed the heads and the exit count
+        hipLaunchKernelGGL(hg_check_zeroed, dim3((HG_QUEUE_BYTES / 4u + 63u) / 64u), dim3(64), 0, stream,
+                           static_cast<const uint32_t*>(kp.queue), uint32_t(HG_QUEUE_BYTES / 4u), kp.counters + 18);
+#endif
     // deep BLAS (kp.stream_deep): the kDeep thresholds
 #define HG_STREAM_LAUNCH_S(C, M, Q, S)                                                                                 \
     do {                                                                                                               \

@@ -169,6 +169,19 @@ bool mesh_cull_boxes(const hg_mat4& w2l, const BVHEntry& A, const BVHEntry& B, H
     return world_box(l2w, A, dm.cull_a_lo, dm.cull_a_hi) && world_box(l2w, B, dm.cull_b_lo, dm.cull_b_hi);
 }
 
+// A mesh record's exact-cull boxes (its root's two children in world space) and cullable flag, from its matrix; all
+// zero when not cullable, so a partial re-upload leaves no field of the previous matrix behind
+void set_cull_boxes(const HalogenMeshData& m, const BVHEntry* blas, HgDevMesh& dm) {
+    dm.cullable = 0;
+    dm.cull_a_lo = dm.cull_a_hi = dm.cull_b_lo = dm.cull_b_hi = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const uint32_t off = m.accelerationBufferOffset;
+    if (blas[off].triangleCount != 0) return;
+    const BVHEntry& A = blas[off + blas[off].indexA];
+    const BVHEntry& B = blas[off + blas[off].indexA + 1];
+    if (mesh_cull_boxes(m.worldToLocal, A, B, dm)) dm.cullable = 1;
+    else dm.cull_a_lo = dm.cull_a_hi = dm.cull_b_lo = dm.cull_b_hi = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
 // The child-pair record layout (hg_device.h node_pair): q0 = (A.lo, refA), q1 = (A.hi, refB), q2 = (B.lo, -), q3 = (B.hi, -)
 void put_pair(float4* r, const BVHEntry& A, const BVHEntry& B, uint32_t ra, uint32_t rb) {
     r[0] = f4(A.boundingCornerA.x, A.boundingCornerA.y, A.boundingCornerA.z, bits(ra));
@@ -544,13 +557,7 @@ int hg_upload_scene_gen(hg_ctx* c, uint64_t geometry_generation, const HalogenSp
                 return fail(c, HG_E_INVALID, "mesh %d: materialIndex %u out of range", mi, m.materialIndex);
             std::memcpy(dm[mi].w2l, m.worldToLocal.m, sizeof dm[mi].w2l);
             dm[mi].material = m.materialIndex;
-            dm[mi].cullable = 0;
-            const uint32_t off = m.accelerationBufferOffset;
-            if (blas[off].triangleCount == 0) {
-                const BVHEntry& A = blas[off + blas[off].indexA];
-                const BVHEntry& B = blas[off + blas[off].indexA + 1];
-                if (mesh_cull_boxes(m.worldToLocal, A, B, dm[mi])) dm[mi].cullable = 1;
-            }
+            set_cull_boxes(m, blas, dm[mi]);
         }
         if (int rc = set_device(c)) return rc;
         if (int rc = quiesce(c)) return rc;  // no trace in flight reads the buffers replaced below
@@ -684,12 +691,7 @@ int hg_upload_scene_gen(hg_ctx* c, uint64_t geometry_generation, const HalogenSp
         dm[mi].root_ref = root;
         dm[mi].tri_offset = toff;
         dm[mi].material = m.materialIndex;
-        dm[mi].cullable = 0;
-        if (blas[off].triangleCount == 0) {
-            const BVHEntry& A = blas[off + blas[off].indexA];
-            const BVHEntry& B = blas[off + blas[off].indexA + 1];
-            if (mesh_cull_boxes(m.worldToLocal, A, B, dm[mi])) dm[mi].cullable = 1;
-        }
+        set_cull_boxes(m, blas, dm[mi]);
     }
     if (rec.size() / 4 >= (size_t(1) << 26))
         return fail(c, HG_E_UNSUPPORTED, "BLAS too large: %zu device node records", rec.size() / 4);
@@ -1285,6 +1287,12 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 L.blend_pending = e == hipSuccess;
                 done += kc.n_frames;
             }
+            if (e != hipSuccess)  // a sort or a queue launch that failed part way may have left its words non-zero
+                for (hg_ctx::TraceLane& L : c->lanes) {
+                    if (L.queue.p) (void)hipMemsetAsync(L.queue.p, 0, L.queue.bytes, L.stream);
+                    if (L.order_scratch.p) (void)hipMemsetAsync(L.order_scratch.p, 0, L.order_scratch.bytes, L.stream);
+                    L.tile_cost_valid = L.tile_order_valid = false;
+                }
         } else if (regen) {  // a regenerating launch that blends in the kernel (make noitems): on the context stream
             HgKernelParams kc = kp;
             for (int done = 0; done < n_frames && e == hipSuccess;) {

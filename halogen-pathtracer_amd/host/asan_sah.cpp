@@ -4,9 +4,12 @@
 //
 //   asan_sah N_TRIS SEED
 // builds the SAH tree of a random triangle soup, of a flat grid (every box thin), of coincident triangles (every
-// centroid equal) and of an empty mesh, and checks every triangle lands in exactly one leaf.
+// centroid equal), of denormal and near-FLT_MAX coordinates (a bin scale of inf or 0) and of an empty mesh, and checks
+// every triangle lands in exactly one leaf; a NaN or infinite vertex is an invalid argument.
+// Built with -fsanitize=float-cast-overflow too: no float -> int bin conversion may be out of range.
 #include <cstdio>
 #include <cstdlib>
+#include <limits>
 #include <random>
 #include <vector>
 
@@ -77,5 +80,26 @@ int main(int argc, char** argv) {
     }
     if ((rc = check("coincident", same, 100, 2))) return rc;
     if ((rc = check("empty", same, 0, 2))) return rc;
+    std::vector<float> tiny(soup), huge(soup);  // centroid spans of ~1e-38 (scale inf) and ~3e38 (extent inf)
+    for (size_t i = 0; i < soup.size(); ++i) {
+        tiny[i] = soup[i] * 1e-39f;
+        huge[i] = (soup[i] - 5.0f) * 6e37f;
+    }
+    if ((rc = check("denormal", tiny, n_tris, 2))) return rc;
+    if ((rc = check("huge", huge, n_tris, 2))) return rc;
+    for (const float bad : {std::numeric_limits<float>::quiet_NaN(), std::numeric_limits<float>::infinity()}) {
+        std::vector<float> v(soup);
+        v[v.size() / 2] = bad;
+        std::vector<int32_t> idx(size_t(n_tris) * 3 + 3);
+        for (size_t i = 0; i < idx.size(); ++i) idx[i] = int32_t(i % (v.size() / 3));
+        std::vector<BVHEntry> nodes(size_t(2 * n_tris + 2));
+        const int64_t n = hg_build_blas_sah(v.data(), int32_t(v.size() / 3), idx.data(), n_tris, 2, 48, nodes.data(),
+                                            int64_t(nodes.size()));
+        if (n != HG_E_INVALID) {
+            std::fprintf(stderr, "non-finite vertex: returned %lld\n", (long long)n);
+            return 7;
+        }
+        std::printf("non-finite vertex rejected\n");
+    }
     return 0;
 }

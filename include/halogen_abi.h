@@ -167,8 +167,9 @@ typedef struct hg_counters {
                               two trace streams overlap, so trace_ms counts shared time twice; trace_busy_ms /
                               trace_launches is the kernel's device time per launch */
     uint64_t order_faults; /* HG_CHECK_EXEC builds only: cost-order sorts whose output was not a permutation of the tiles
-                              (a placement out of range, or a tile placed other than once); must stay 0.  0 in product
-                              builds */
+                              (a placement out of range, or a tile placed other than once), and words of a sort's
+                              scratch or a queue launch's heads found non-zero when the next use starts; must stay 0.
+                              0 in product builds */
     uint64_t scene_uploads;         /* hg_upload_scene calls that (re)built the device scene, since hg_create */
     uint64_t scene_uploads_skipped; /* ... and calls whose five arrays equalled the last upload's byte for byte, which
                                        change nothing and return at once (the reference re-uploads on every camera

@@ -104,3 +104,50 @@ def test_gpu_partial_reupload_equals_full(gpu, name):
         cnt = ctx.counters()
     assert cnt["scene_uploads"] == 2 and cnt["scene_uploads_partial"] == 1 and cnt["scene_uploads_skipped"] == 0, cnt
     assert_bitwise(img, want, f"{name}: partial re-upload vs a fresh full upload")
+
+
+def _with_spheres(packed, n):
+    """The same scene with its first n spheres (the sphere buffer's length changes; triangles and BVH as before)."""
+    out = _copy(packed)
+    out.spheres = (type(packed.spheres)._type_ * n)(*[packed.spheres[i] for i in range(n)])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dragon1_64x36", "c1_64"])
+def test_gpu_partial_reupload_sphere_count_and_cull_flip(gpu, name):
+    """A partial re-upload (triangles and BVH entries unchanged) that (a) drops a sphere, so the sphere buffer shrinks
+    and the params' sphere count follows, and (b) gives a mesh a world->local matrix too close to singular to invert,
+    so its world-space cull boxes are dropped (cullable 1 -> 0) and every field of its old record must be rebuilt from
+    the new matrix: each render equals a fresh context's full upload of the same arrays, bit for bit."""
+    packed, params, cube, frames, acc = cases.setup(name)
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    fewer = _with_spheres(packed, len(packed.spheres) - 1)
+    singular = _copy(packed)
+    for i in (0, 1, 2, 4, 5, 6, 8, 9, 10):  # the linear part scaled by 1e-11: |det| ~ 1e-33 (hg_runtime.hip invert4)
+        singular.meshes[0].worldToLocal.m[i] = np.float32(singular.meshes[0].worldToLocal.m[i] * 1e-11)
+    for variant, what in ((fewer, "one sphere fewer"), (singular, "a mesh no longer cullable"),
+                          (packed, "back to the first scene")):
+        vparams = cases.setup(name)[1]
+        vparams.bufferCounts = abi.Vec4(len(variant.spheres), len(variant.meshes), 0.0, 0.0)
+        want, wcnt = gpu_render(variant, vparams, 3, True, cube)
+        with abi.Context(0) as ctx:
+            ctx.upload_scene(packed)
+            if cube is not None:
+                ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+            ctx.resize(W, H)
+            ctx.set_params(params)
+            ctx.render(2, True)
+            if variant is packed:  # a round trip through both changes, back to the first arrays
+                ctx.upload_scene(singular)
+                ctx.render(1, True)
+                ctx.upload_scene(fewer)
+                ctx.render(1, True)
+            ctx.upload_scene(variant)
+            ctx.clear_accumulation()
+            ctx.set_params(vparams)
+            ctx.render(3, True)
+            img = ctx.readback(W, H)
+            cnt = ctx.counters()
+        assert cnt["scene_uploads_partial"] >= 1 and cnt["scene_uploads_skipped"] == 0, (what, cnt)
+        assert_bitwise(img, want, f"{name}: partial re-upload, {what}")

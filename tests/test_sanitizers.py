@@ -101,7 +101,10 @@ def test_host_pool_under_tsan(tmp_path):
 
 def test_sah_builder_under_asan_ubsan():
     """hg_build_blas_sah (the non-reference SAH hierarchy, csrc/hg_host.cpp) under AddressSanitizer + UBSan: random
-    soups, a flat grid (every box thin, padded), coincident triangles, an empty mesh; every triangle in one leaf."""
+    soups, a flat grid (every box thin, padded), coincident triangles, an empty mesh, denormal and near-FLT_MAX
+    coordinates (-fsanitize=float-cast-overflow: no bin conversion out of range); every triangle in one leaf; a NaN or
+    infinite vertex rejected."""
     subprocess.run(["make", "-s", "-C", str(ROOT / "halogen-pathtracer_amd"), "asan_sah"], check=True)
     out = run([ASAN_SAH, 20000, 7])
-    assert out.count("every triangle in one leaf") == 10, out
+    assert out.count("every triangle in one leaf") == 12, out
+    assert out.count("non-finite vertex rejected") == 2, out
