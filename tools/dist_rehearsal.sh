@@ -1,6 +1,7 @@
 #!/bin/bash
 # Rehearsal of bench.py's N-rank path on ONE GPU: 2 (or 3) ranks over gloo, every rank on device 0.  The gathered
-# image of N ranks x F frames must equal the 1-rank image of N*F frames (weak scaling semantics), bit for bit.
+# image of N ranks x F frames must equal the 1-rank image of N*F frames (weak scaling semantics), bit for bit; the
+# strong-scaling leg's gathered image (one image's tiles over the N ranks) must equal one context's, bit for bit.
 set -u
 mkdir -p gpurun_out/dist
 export HALOGEN_BENCH_DEVICE=0
@@ -20,6 +21,14 @@ a = np.load('gpurun_out/dist/img_n$n.npy'); b = np.load('gpurun_out/dist/img_1x$
 same = a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 print('n=$n gathered image bit-identical to 1-rank render:', same, a.shape)
 sys.exit(0 if same else 1)" || exit 1
+  python -c "
+import json, sys
+r = json.loads(open('gpurun_out/dist/bench_n$n.json').read().strip().splitlines()[-1])
+st = r.get('strong_scaling') or {}
+print('n=$n weak', r['value'], '| strong', st.get('value'), st.get('ms_per_step'), 'balance', st.get('trace_balance'),
+      'tiles', [x['tiles'] for x in st.get('per_rank', [])], '| strong gathered bit-identical:',
+      st.get('gathered_bit_identical_to_one_context'))
+sys.exit(0 if st.get('gathered_bit_identical_to_one_context') else 1)" || exit 1
 done
 # the default transport (hg_comm over RCCL) cannot join two ranks on one GPU (RCCL refuses a duplicate device): every
 # rank must agree to time the torch gather instead, report why, and still gather the same image
