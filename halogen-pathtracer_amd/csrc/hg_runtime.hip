@@ -804,6 +804,19 @@ int render_check(hg_ctx* c, int32_t n_frames) {
     return HG_OK;
 }
 
+// The server had work a moment ago: the blend of its last posted frame has not run yet, so that frame's gate has not
+// passed (or has just passed) and the waves tracing its last units live on for the kernel's idle time after them.
+// (Assumes the context stream never holds the gate back for anything near that long: the work queued there ahead of
+// it is other gates, blends, clears and readbacks.)
+bool server_recently_busy(const hg_ctx::Server& S) {
+    if (S.posted == 0u) return false;
+    const uint32_t s = (S.posted - 1u) & (S.ring_n - 1u);
+    if (!S.blend_valid[s]) return false;
+    const hipError_t q = hipEventQuery(S.blended[s]);
+    (void)hipGetLastError();  // hipErrorNotReady is a status here
+    return q == hipErrorNotReady;
+}
+
 // The server can take the frame of FrameCount `fc` next: running, started with these parameters and options, `fc`
 // continuing its chain, room left in its lifetime's unit numbering, not idle for long and its kernel still resident
 bool server_continues(hg_ctx* c, int32_t fc) {
@@ -813,7 +826,7 @@ bool server_continues(hg_ctx* c, int32_t fc) {
     p.frameCount = S.params.frameCount;
     if (std::memcmp(&p, &S.params, sizeof p) != 0 || int64_t(fc) != int64_t(S.params.frameCount) + int64_t(S.posted) ||
         S.kernel_variant != c->kernel || S.descent_t != c->descent_t || S.posted >= S.cap ||
-        host_seconds() - S.last_post_s >= kServerIdleS)
+        (host_seconds() - S.last_post_s >= kServerIdleS && !server_recently_busy(S)))
         return false;
     const hipError_t q = hipStreamQuery(S.stream);
     (void)hipGetLastError();
@@ -863,13 +876,16 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
             rc = fail(c, HG_E_HIP, "hipMemsetAsync(server order scratch) failed");
     }
     if (rc) return rc;
+    // The counts and heads are zeroed on the context stream: after the last lifetime's gates and blends, and before
+    // this lifetime's gates, which are queued there too (zeroed on the server's stream instead, a new gate could read
+    // the last lifetime's count of its ring slot before the zeroing and pass at once)
+    HG_HIP(c, hipMemsetAsync(S.ctl.p, 0, HG_SV_CTL_BYTES, c->stream));
+    HG_HIP(c, hipMemsetAsync(S.done.p, 0, size_t(ring) * 128u, c->stream));
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (int r = event_pair(c, ev)) return r;
     HG_HIP(c, hipEventRecord(ev.first, c->stream));
     HG_HIP(c, hipStreamWaitEvent(S.stream, ev.first, 0));
     c->free_events.push_back(ev);
-    HG_HIP(c, hipMemsetAsync(S.ctl.p, 0, HG_SV_CTL_BYTES, S.stream));
-    HG_HIP(c, hipMemsetAsync(S.done.p, 0, size_t(ring) * 128u, S.stream));
     HgKernelParams kp = kp_in;
     kp.tile_order = nullptr;
     kp.tile_cost = nullptr;
@@ -939,7 +955,7 @@ int server_post(hg_ctx* c) {
     const uint32_t k = S.posted, s = k & (S.ring_n - 1u);
     if (S.blend_valid[s]) {
         HG_HIP(c, hipEventSynchronize(S.blended[s]));
-        if (host_seconds() - S.last_post_s >= kServerIdleS) return HG_E_UNSUPPORTED;
+        if (host_seconds() - S.last_post_s >= kServerIdleS && !server_recently_busy(S)) return HG_E_UNSUPPORTED;
     }
     S.uses[s]++;
     const uint32_t tiles = uint32_t(c->n_local_tiles), n_slots = tiles * 64u;

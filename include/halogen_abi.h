@@ -209,8 +209,7 @@ enum {
 enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG_KERNEL_MEGA_STREAM = 3,
        HG_KERNEL_MEGA_POOL = 4, HG_KERNEL_AUTO = 5 };
 /* HG_OPT_BLOCK: workgroup size of the lockstep kernel HG_KERNEL_MEGA (64/128/256; the debug views, large-maxBounces
- *   fallback) and of the wavefront trace kernel; the regenerating / streaming / pool kernels always run one-wave
- *   workgroups (their per-lane LDS rows assume it) and ignore it.  HG_OPT_COUNTERS: work counters on/off.
+ *   fallback); the regenerating / streaming kernels always run one-wave workgroups (their per-lane LDS rows assume it) and ignore it.  HG_OPT_COUNTERS: work counters on/off.
  * HG_OPT_TIMING: time every traversal-kernel launch with HIP events (hg_counters.trace_ms).
  * HG_OPT_REFILL: (the removed wavefront pipeline's dequeue threshold) returns HG_E_UNSUPPORTED.
  * HG_OPT_FRAME_SPLIT: regenerating kernel, waves per tile that trace disjoint frame ranges (their colours are then

@@ -97,7 +97,8 @@ def test_gpu_server_many_frames_match_batched(gpu, frames):
                 img = np.full((H, W, 4), np.nan, np.float32)
                 ctx.readback(W, H, img)
                 cnt = ctx.counters()
-            assert_bitwise(img, ref, f"{frames} frames, {per_call} per call, tiling {tiling}")
+            assert_bitwise(img, ref, f"{frames} frames, {per_call} per call, tiling {tiling}, "
+                                     f"{cnt['server_launches']} server launches")
             assert cnt["server_frames"] == frames and cnt["paths"] == rc["paths"], cnt
 
 
@@ -138,7 +139,8 @@ def test_gpu_server_restarts_keep_the_image(gpu):
     """Every event that ends a server lifetime, mid-run, against the same call sequence with the server off: a camera
     move (set_params with a new camera and FrameCount 1, then clear, as ClearAccumulation does, RP:262-268), a
     checkpoint (set_accumulation), a clear alone (the server keeps running: the clear is ordered between blends), a
-    counters read, a launch of another kind (a 16-frame call), an idle gap longer than the server's, an upload."""
+    counters read, a launch of another kind (a 16-frame call), an idle gap longer than the server's, idle gaps that
+    restart a server still running (its counts not zero), an upload."""
     packed, params, cube, _, _ = cases.setup("dragon10_64x36")
     moved = cases.setup("dragon10_64x36")[1]
     moved.camLocalToWorld.m[12] += 0.05
@@ -165,6 +167,9 @@ def test_gpu_server_restarts_keep_the_image(gpu):
             frames(2)
             time.sleep(0.08)
             frames(2)
+            for _ in range(3):  # idle gaps past the host's restart threshold, well inside the waves' idle time: a
+                time.sleep(0.03)  # restart over a live server whose ring-slot counts are not zero
+                frames(3)
             ctx.upload_scene(packed)
             frames(2)
             cnt = ctx.counters()
