@@ -143,7 +143,8 @@
 // host word) and the host-poll ticket (u64 s_memrealtime: one wave reads the host word per HG_SV_POLL_TICKS).
 #define HG_SV_MIRROR_WORD 288u
 #define HG_SV_TICKET_WORD 320u
-#define HG_SV_CTL_BYTES (11u * 128u)
+#define HG_SV_EXIT_WORD 352u    // (diagnostics) waves of the server that left | grid << 32
+#define HG_SV_CTL_BYTES (12u * 128u)
 #ifndef HG_SV_POLL_TICKS
 #define HG_SV_POLL_TICKS 50u  // 0.5 us between reads of the host word over PCIe, for the whole GPU
 #endif

@@ -1014,8 +1014,8 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
     uint32_t u = lds_get(hg_sv.pend);
     uint32_t view = lds_get(hg_sv.view);
     if (u == HG_NONE) {
-        if (view == lds_get(hg_sv.dry)) {  // every head was dry at this view: anything new posted?
-            view = sv_view(kp);
+        if (view == lds_get(hg_sv.dry)) {  // every head was dry at this view: anything new posted?  (A busy wave
+            view = sv_poll(kp);            // polls the host word too: no wave may be waiting to do it)
             if (view == lds_get(hg_sv.dry)) return;
         }
         const uint32_t x = blockIdx.x & 7u;
@@ -1388,6 +1388,12 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     }
     if constexpr (kQueue) record_tile_cost(lane);
     else items.record_cost(kp, lane);
+    if constexpr (kServer) {  // (diagnostics, hg_destroy under HALOGEN_SERVER_TRACE) waves out | grid << 32
+        if (lane == 0u) {
+            __hip_atomic_store(kp.queue + HG_SV_EXIT_WORD + 1u, gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(kp.queue + HG_SV_EXIT_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if constexpr (kQueue && !kServer) {
         // The last wave out resets the queue heads for the next launch on this stream (no memset launch per queue
         // launch: a blit kernel waited for a CU that the other streams' persistent waves held).  A wave leaves only

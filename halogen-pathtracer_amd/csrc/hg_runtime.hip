@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -291,6 +292,27 @@ double host_seconds() {
 constexpr double kServerIdleS = 0.020;
 constexpr uint32_t kServerIdleTicks = 20000000u;           // 200 ms of the 100-MHz s_memrealtime
 constexpr uint64_t kGateTimeoutTicks = 30ull * 100000000ull;  // a frame's gate gives up after 30 s (reported)
+// (HALOGEN_SERVER_GATE_TIMEOUT_MS overrides it, for diagnostics: a shorter bound turns a lost frame into an error fast)
+uint64_t gate_timeout_ticks() {
+    static const uint64_t t = [] {
+        const char* e = std::getenv("HALOGEN_SERVER_GATE_TIMEOUT_MS");
+        const long long ms = e ? std::atoll(e) : 0;
+        return ms > 0 ? uint64_t(ms) * 100000ull : kGateTimeoutTicks;
+    }();
+    return t;
+}
+
+// HALOGEN_SERVER_TRACE=1: every server start, stop, post and refusal on stderr (diagnostics)
+void sv_trace(const char* fmt, ...) {
+    static const bool on = std::getenv("HALOGEN_SERVER_TRACE") != nullptr;
+    if (!on) return;
+    va_list ap;
+    va_start(ap, fmt);
+    std::fprintf(stderr, "[hg server %.6f] ", host_seconds());
+    std::vfprintf(stderr, fmt, ap);
+    std::fputc('\n', stderr);
+    va_end(ap);
+}
 
 // A gate's timeout (the frame's count never reached its target) reported once, as an error of the entry point
 int server_check(hg_ctx* c) {
@@ -307,6 +329,7 @@ int server_stop(hg_ctx* c) {
     if (!S.running) return HG_OK;
     __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted) | HG_SV_STOP, __ATOMIC_SEQ_CST);
     const double t0 = host_seconds();
+    sv_trace("stop: %u frames posted", S.posted);
     hipError_t q;
     while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
         if (host_seconds() - t0 > 60.0) {
@@ -317,6 +340,7 @@ int server_stop(hg_ctx* c) {
     }
     (void)hipGetLastError();  // hipErrorNotReady is a status here
     S.running = false;
+    sv_trace("stopped after %.3f ms (%s)", (host_seconds() - t0) * 1e3, hipGetErrorString(q));
     if (q != hipSuccess) return fail(c, HG_E_HIP, "render server: %s", hipGetErrorString(q));
     return server_check(c);
 }
@@ -427,18 +451,19 @@ void hg_destroy(hg_ctx* c) {
     c->pending_frames = 0;  // held frames are discarded: nothing can observe them after this call
     (void)hipSetDevice(c->device);
     (void)server_stop(c);
+    sv_trace("destroy: server stopped");
+    if (std::getenv("HALOGEN_SERVER_TRACE")) {
+        unsigned long long w[4] = {};
+        if (c->sv.ctl.p && hipMemcpyAsync(w, static_cast<char*>(c->sv.ctl.p) + HG_SV_EXIT_WORD * 4u, sizeof w,
+                                          hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess)
+            sv_trace("destroy: server waves out %llu of %llu", w[0] & 0xFFFFFFFFull, w[0] >> 32);
+        sv_trace("destroy: device synchronize %s", hipGetErrorString(hipDeviceSynchronize()));
+    }
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    sv_trace("destroy: context stream idle");
     for (hg_ctx::TraceLane& L : c->lanes)
         if (L.stream) (void)hipStreamSynchronize(L.stream);
-    {
-        hg_ctx::Server& S = c->sv;
-        if (S.stream) (void)hipStreamSynchronize(S.stream);
-        for (DevBuf* b : {&S.ctl, &S.done, &S.ring, &S.spill, &S.tile_cost, &S.tile_order, &S.order_scratch}) release(*b);
-        for (hipEvent_t& e : S.blended)
-            if (e) (void)hipEventDestroy(e);
-        if (S.host) (void)hipHostFree(S.host);
-        if (S.stream) (void)hipStreamDestroy(S.stream);
-    }
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tris, &c->normals, &c->cube,
                       &c->acc, &c->counters_dev, &c->spill})
         release(*b);
@@ -448,6 +473,24 @@ void hg_destroy(hg_ctx* c) {
         if (L.traced) (void)hipEventDestroy(L.traced);
         if (L.blended) (void)hipEventDestroy(L.blended);
         if (L.stream) (void)hipStreamDestroy(L.stream);
+    }
+    sv_trace("destroy: trace streams destroyed");
+    // The server's stream after the trace streams: destroyed before them, the next hipStreamDestroy of a plain trace
+    // stream hung (HIP 7.2 on the MI355X box, every time after a 200-frame server run with one frame per call; streams
+    // idle and every server wave out, per HALOGEN_SERVER_TRACE)
+    {
+        hg_ctx::Server& S = c->sv;
+        if (S.stream) (void)hipStreamSynchronize(S.stream);
+        sv_trace("destroy: every stream idle");
+        for (DevBuf* b : {&S.ctl, &S.done, &S.ring, &S.spill, &S.tile_cost, &S.tile_order, &S.order_scratch}) release(*b);
+        sv_trace("destroy: server buffers freed");
+        for (hipEvent_t& e : S.blended)
+            if (e) (void)hipEventDestroy(e);
+        sv_trace("destroy: server events destroyed");
+        if (S.host) (void)hipHostFree(S.host);
+        sv_trace("destroy: server host word freed");
+        if (S.stream) (void)hipStreamDestroy(S.stream);
+        sv_trace("destroy: server stream destroyed");
     }
     if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
     release(c->image);
@@ -462,6 +505,7 @@ void hg_destroy(hg_ctx* c) {
     for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->free_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    sv_trace("destroy: done");
     delete c;
 }
 
@@ -943,6 +987,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     S.kp = kp;
     S.last_post_s = host_seconds();
     c->server_launches++;
+    sv_trace("start: FrameCount %d, %u tiles, ring %u, grid %u", fc, tiles, ring, grid);
     return HG_OK;
 }
 
@@ -954,7 +999,9 @@ int server_post(hg_ctx* c) {
     hg_ctx::Server& S = c->sv;
     const uint32_t k = S.posted, s = k & (S.ring_n - 1u);
     if (S.blend_valid[s]) {
+        sv_trace("post %u: waiting for the blend of frame %u", k, k - S.ring_n);
         HG_HIP(c, hipEventSynchronize(S.blended[s]));
+        sv_trace("post %u: waited", k);
         if (host_seconds() - S.last_post_s >= kServerIdleS && !server_recently_busy(S)) return HG_E_UNSUPPORTED;
     }
     S.uses[s]++;
@@ -964,7 +1011,7 @@ int server_post(hg_ctx* c) {
     HG_HIP(c, hg_launch_server_frame(static_cast<float4*>(c->acc.p),
                                      static_cast<const float4*>(S.ring.p) + size_t(s) * n_slots, n_slots,
                                      S.kp.first_frame + int32_t(k), static_cast<const uint32_t*>(S.done.p) + 32u * s,
-                                     S.uses[s] * tiles, kGateTimeoutTicks, static_cast<unsigned long long*>(err),
+                                     S.uses[s] * tiles, gate_timeout_ticks(), static_cast<unsigned long long*>(err),
                                      c->stream));
     HG_HIP(c, hipEventRecord(S.blended[s], c->stream));
     S.blend_valid[s] = true;
@@ -972,6 +1019,7 @@ int server_post(hg_ctx* c) {
     __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted), __ATOMIC_SEQ_CST);
     S.last_post_s = host_seconds();
     c->server_frames++;
+    sv_trace("posted %u (slot %u, target %u)", k, s, S.uses[s] * tiles);
     return HG_OK;
 }
 
