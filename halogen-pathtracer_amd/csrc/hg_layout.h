@@ -138,15 +138,21 @@
 // 128-B line): the last wave out zeroes them for the next launch (the runtime zeroes the buffer once, at allocation)
 #define HG_QUEUE_DONE_WORD 256u
 #define HG_QUEUE_BYTES (9u * 128u)
-// The render server's control block (kp.queue of a server launch, zeroed before it): the 8 unit heads as above, then on
-// lines of their own the device mirror of the host's post word (u64, raised by atomic max by whichever wave reads the
-// host word) and the host-poll ticket (u64 s_memrealtime: one wave reads the host word per HG_SV_POLL_TICKS).
+// Render server control words (kp.queue of a server launch, HG_SV_CTL_BYTES, zeroed at each server start), each on a
+// 128-B line of its own: the 8 unit heads (as above), then HG_SV_MIRRORS copies of the device mirror of the host's post
+// word (u64, raised by atomic max by whichever wave read the host word; an idle
+// wave reads copy blockIdx.x % HG_SV_MIRRORS: the polling of thousands of idle waves spread over as many lines), one
+// host-poll ticket per XCD (blockIdx.x % 8), and the count of waves that left (diagnostics)
+#define HG_SV_MIRRORS 16u
 #define HG_SV_MIRROR_WORD 288u
-#define HG_SV_TICKET_WORD 320u
-#define HG_SV_EXIT_WORD 352u    // (diagnostics) waves of the server that left | grid << 32
-#define HG_SV_CTL_BYTES (12u * 128u)
+#define HG_SV_TICKET_WORD (HG_SV_MIRROR_WORD + 32u * HG_SV_MIRRORS)
+#define HG_SV_EXIT_WORD (HG_SV_TICKET_WORD + 32u * 8u)  // waves of the server that left | grid << 32
+#define HG_SV_CTL_BYTES ((HG_SV_EXIT_WORD + 32u) * 4u)
 #ifndef HG_SV_POLL_TICKS
-#define HG_SV_POLL_TICKS 50u  // 0.5 us between reads of the host word over PCIe, for the whole GPU
+#define HG_SV_POLL_TICKS 200u  // 2 us between reads of the host word over PCIe, per XCD
+#endif
+#ifndef HG_SV_WAVES
+#define HG_SV_WAVES 4  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
 #endif
 #ifndef HG_SV_RING
 #define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most

@@ -915,9 +915,10 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
 //             word itself (a ticket) and raises the mirror by atomic max.
 //   frames    a wave counts, per frame in a window of 4 (LDS), the units it pulled and the items of them its lanes
 //             finished; once they match, after a store drain, it adds the units to the frame's ring-slot count
-//             (frames_done).  Colours go to the frame's ring slot with write-through (sc1) stores: the gate kernel on
-//             the context stream waits for the count (sc1 loads), and the blend after it reads them with sc1 loads
-//             (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + drain + agent atomic / sc1 loads).
+//             (frames_done).  Colours go to the frame's ring slot, and the ring and the counts are uncached device
+//             memory (no XCD's L2 holds their lines): the gate kernel on the context stream waits for the count, and
+//             the blend after it reads the colours, whichever XCD wrote them (plain stores then the drain, then the
+//             count's atomic: the colours are in memory before the count says so).
 //   leaving   a wave with no item and no posted unit left waits (s_sleep); it leaves once the stop flag is set and
 //             nothing posted is left to claim, or after sv_idle_ticks with nothing posted (the host restarts a server
 //             that has been idle for less than half of that instead of posting to it).
@@ -981,8 +982,8 @@ __device__ __forceinline__ uint32_t sv_units(unsigned long long w) {
 // Refresh the view from the device mirror of the post word
 __device__ uint32_t sv_view(const HgKernelParams& kp) {
     uint32_t v = lds_get(hg_sv.view);
-    const unsigned long long m = __hip_atomic_load(sv_word64(kp, HG_SV_MIRROR_WORD), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long m = __hip_atomic_load(
+        sv_word64(kp, HG_SV_MIRROR_WORD + 32u * (blockIdx.x % HG_SV_MIRRORS)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t u = sv_units(m);
     if (u > v) {
         v = u;
@@ -991,10 +992,10 @@ __device__ uint32_t sv_view(const HgKernelParams& kp) {
     if (m & HG_SV_STOP) lds_put(hg_sv.stop, 1u);
     return v;
 }
-// (idle waves) take the host-poll ticket if it is free, read the host word over PCIe (system scope) and raise the
-// mirror; then refresh the view
+// Take this XCD's host-poll ticket if it is free, read the host word over PCIe (system scope) and raise every mirror
+// copy; then refresh the view.  (Idle waves call it every few spins, busy ones when they find the heads dry.)
 __device__ uint32_t sv_poll(const HgKernelParams& kp) {
-    unsigned long long* const ticket = sv_word64(kp, HG_SV_TICKET_WORD);
+    unsigned long long* const ticket = sv_word64(kp, HG_SV_TICKET_WORD + 32u * (blockIdx.x & 7u));
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     unsigned long long t = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (now >= t && __hip_atomic_compare_exchange_strong(ticket, &t, now + HG_SV_POLL_TICKS, __ATOMIC_RELAXED,
@@ -1002,7 +1003,9 @@ __device__ uint32_t sv_poll(const HgKernelParams& kp) {
         const unsigned long long h = __hip_atomic_load(
             sv_ptr<const unsigned long long>(lds_get(hg_sv.post_lo), lds_get(hg_sv.post_hi)), __ATOMIC_RELAXED,
             __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_fetch_max(sv_word64(kp, HG_SV_MIRROR_WORD), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t m = 0; m < HG_SV_MIRRORS; ++m)
+            __hip_atomic_fetch_max(sv_word64(kp, HG_SV_MIRROR_WORD + 32u * m), h, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     }
     return sv_view(kp);
 }
@@ -1066,7 +1069,7 @@ __device__ void sv_flush() {
     for (uint32_t w = 0; w < 4u; ++w) {
         const uint32_t n = lds_get(hg_sv.win_units[w]);
         if (n == 0u || lds_get(hg_sv.win_done[w]) != lds_get(hg_sv.win_items[w])) continue;
-        if (!drained) {  // every lane's write-through colour stores complete before the count moves
+        if (!drained) {  // every lane's colour stores complete before the count moves
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             __builtin_amdgcn_s_waitcnt(0);
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1103,29 +1106,28 @@ __device__ bool sv_refill(const HgKernelParams& kp) {
 __device__ uint32_t sv_wait(const HgKernelParams& kp) {
     hg_wave_cost[threadIdx.x >> 6] = nullptr;  // the wait is no tile's cost
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t seen = HG_NONE;  // the view at which the heads were last read
     for (uint32_t spin = 0;; ++spin) {
-        const uint32_t view = sv_poll(kp);
+        // one coherent load per spin (this wave's mirror copy); the host word through the ticket every 4th spin
+        const uint32_t view = (spin & 3u) == 0u ? sv_poll(kp) : sv_view(kp);
         const uint32_t pend = lds_get(hg_sv.pend);
         bool open = pend != HG_NONE && pend < view;
-        for (uint32_t h = 0; h < 8u && !open; ++h) open = h + 8u * ld_agent(kp.queue + 32u * h) < view;
+        if (!open && view != seen) {  // the heads, only when the posted units changed
+            seen = view;
+            for (uint32_t h = 0; h < 8u && !open; ++h) open = h + 8u * ld_agent(kp.queue + 32u * h) < view;
+        }
         if (open) {
             lds_put(hg_sv.dry, HG_NONE);
             return 0u;
         }
         if (lds_get(hg_sv.stop)) return 1u;  // the final post word: nothing posted is left to claim
         if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(lds_get(hg_sv.idle_ticks))) return 1u;
-        if (spin < 64u) __builtin_amdgcn_s_sleep(2);
-        else __builtin_amdgcn_s_sleep(16);
+        // about 0.2 us between the first polls, then about 3.4 us (s_sleep counts 64 clocks)
+        if (spin < 16u) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(127);
     }
 }
-// Write-through colour store of a server frame (8-B sc1 stores: device-coherent at the memory side)
-__device__ __forceinline__ void fc_store_wt(float4* p, float4 v) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-    __hip_atomic_store(q, (static_cast<unsigned long long>(__float_as_uint(v.y)) << 32) | __float_as_uint(v.x),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (static_cast<unsigned long long>(__float_as_uint(v.w)) << 32) | __float_as_uint(v.z),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// (the colour stores of a server frame: fc_store into the uncached ring)
 
 // Streaming variant (HG_KERNEL_MEGA_STREAM): the regenerating kernel with a resumable traversal.  Lanes advance
 // their traversal one while-while round at a time; once at most HG_STREAM_TMIN lanes are still traversing (and
@@ -1316,8 +1318,9 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                         if constexpr (kServer) {
                             if (!fresh) {
                                 const uint32_t k = smp.frame - uint32_t(kp.first_frame);  // the server's frame index
-                                fc_store_wt(kp.frame_color + size_t(k & lds_get(hg_sv.mask)) * (lds_get(hg_sv.nlt) * 64u) + slot_i,
-                                            make_float4(color.x, color.y, color.z, 1.0f));
+                                // (the ring is uncached memory: the gate and blend on another XCD read what this wrote)
+                                fc_store(kp.frame_color + size_t(k & lds_get(hg_sv.mask)) * (lds_get(hg_sv.nlt) * 64u) + slot_i,
+                                         make_float4(color.x, color.y, color.z, 1.0f));
                                 atomicAdd(&hg_sv.win_done[k & 3u], 1u);  // (LDS) one more item of frame k finished
                             }
                         } else if (!fresh) {
@@ -1480,9 +1483,9 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
 }
 
 // The render server's per-frame work on the context stream (hg_runtime.hip server_post): the gate waits until the
-// frame's ring-slot count reaches `target` (one wave; sc1 polls with a sleep, bounded: after `timeout_ticks` it
-// records the failure in the host-visible error word and returns), then the blend reads the frame's colours with sc1
-// loads (written through by the server's waves) and blends them into the accumulator: acc*(1-w) + c*w, w = 1/FrameCount
+// frame's ring-slot count reaches `target` (one wave; agent-scope polls with a sleep, bounded: after `timeout_ticks`
+// it records the failure in the host-visible error word and returns), then the blend reads the frame's colours from
+// the uncached ring and blends them into the accumulator: acc*(1-w) + c*w, w = 1/FrameCount
 // (AccumulationShader.shader:33), the same operations as every other blend.  Both fit beside the server's waves
 // (64-thread groups, no LDS, few registers).
 __global__ __launch_bounds__(64) void hg_server_gate(const uint32_t* __restrict__ done, uint32_t target,
@@ -1502,11 +1505,7 @@ __global__ __launch_bounds__(64) void hg_server_blend(float4* __restrict__ acc, 
                                                       uint32_t n_slots, int32_t frame_count) {
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n_slots) return;
-    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(colors + i);
-    const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float4 c = make_float4(__uint_as_float(uint32_t(lo)), __uint_as_float(uint32_t(lo >> 32)),
-                                 __uint_as_float(uint32_t(hi)), __uint_as_float(uint32_t(hi >> 32)));
+    const float4 c = fc_load(colors + i);  // (uncached memory: the server's stores, whichever XCD made them)
     float4 a = acc[i];
     const float w = rcp_exact(float(uint32_t(frame_count)));
     const float k = 1.0f - w;

@@ -281,6 +281,20 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     return HG_OK;
 }
 
+// The same in uncached device memory (MTYPE UC: no L2 holds its lines, so writes from one XCD are seen by loads from
+// any other without cache maintenance): the render server's colour ring and frame counts, written by persistent
+// waves and read by the gate and blend kernels while those waves still run
+int ensure_uncached(hg_ctx* c, DevBuf& b, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 16);
+    if (b.bytes >= bytes) return HG_OK;
+    release(b);
+    hipError_t e = hipExtMallocWithFlags(&b.p, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess)
+        return fail(c, HG_E_NOMEM, "hipExtMallocWithFlags(%zu, uncached) failed: %s", bytes, hipGetErrorString(e));
+    b.bytes = bytes;
+    return HG_OK;
+}
+
 double host_seconds() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -898,7 +912,15 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     const size_t per_frame = size_t(tiles) * 64u * sizeof(float4);
     uint32_t ring = HG_SV_RING;
     while (ring > 2u && size_t(ring) * per_frame > (size_t(2) << 30)) ring >>= 1;
-    const uint32_t slots = uint32_t(c->n_cu) * 4u * HG_STREAM_WAVES;
+    // waves per SIMD: fewer than the kernel's HG_STREAM_WAVES, so that the kernels the context stream runs between the
+    // server's frames (gates, blends, the display untile / pack) find registers and wave slots beside its persistent
+    // waves (HALOGEN_SERVER_WAVES overrides, 1..HG_STREAM_WAVES, for A/B)
+    static const uint32_t sv_waves = [] {
+        const char* e = std::getenv("HALOGEN_SERVER_WAVES");
+        const int v = e ? std::atoi(e) : 0;
+        return uint32_t(v >= 1 && v <= HG_STREAM_WAVES ? v : HG_SV_WAVES);
+    }();
+    const uint32_t slots = uint32_t(c->n_cu) * 4u * sv_waves;
     const uint32_t grid = std::min(tiles, slots);
     const uint32_t lds_part = HG_STREAM_LDS_STACK;
     const size_t spill_bytes = kp_in.stack_depth > lds_part ? size_t(grid) * 64u * (kp_in.stack_depth - lds_part) * 4u : 0;
@@ -907,8 +929,8 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     // them (an event, no host wait) unless a buffer must move (then the context stream is drained first)
     if (S.ring.bytes < size_t(ring) * per_frame || S.done.bytes < size_t(ring) * 128u)
         HG_HIP(c, hipStreamSynchronize(c->stream));
-    int rc = ensure(c, S.ring, size_t(ring) * per_frame);
-    if (!rc) rc = ensure(c, S.done, size_t(ring) * 128u);
+    int rc = ensure_uncached(c, S.ring, size_t(ring) * per_frame);
+    if (!rc) rc = ensure_uncached(c, S.done, size_t(ring) * 128u);
     if (!rc) rc = ensure(c, S.ctl, HG_SV_CTL_BYTES);
     if (!rc && spill_bytes) rc = ensure(c, S.spill, spill_bytes);
     if (!rc && c->tile_order_on) rc = ensure(c, S.tile_cost, 2 * tb);
