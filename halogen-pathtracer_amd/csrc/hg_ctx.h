@@ -100,6 +100,11 @@ struct hg_ctx {
     } sv;
     int32_t server_on = 1;  // HG_OPT_SERVER
     uint64_t server_launches = 0, server_frames = 0;
+    // The server serves only a host that runs ahead: each render call records call_done[calls & 1] on `stream` after
+    // its frames' blends, so at a call the event of the call before last tells whether the GPU still works on it
+    hipEvent_t call_done[2] = {};
+    bool call_done_valid[2] = {};
+    uint64_t calls = 0;
 
     // counters / timing
     DevBuf counters_dev;

@@ -151,8 +151,14 @@
 #ifndef HG_SV_POLL_TICKS
 #define HG_SV_POLL_TICKS 200u  // 2 us between reads of the host word over PCIe, per XCD
 #endif
+#ifndef HG_SV_SLEEP_LONG  // an idle server wave's wait between polls: HG_SV_SPIN_SHORT spins of s_sleep SHORT, then LONG
+#define HG_SV_SLEEP_SHORT 8
+#define HG_SV_SLEEP_LONG 127
+#define HG_SV_SPIN_SHORT 16u
+#define HG_SV_POLL_EVERY 4u  // an idle wave reads the host word (if its XCD's ticket is free) every this many spins
+#endif
 #ifndef HG_SV_WAVES
-#define HG_SV_WAVES 4  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
+#define HG_SV_WAVES 5  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
 #endif
 #ifndef HG_SV_RING
 #define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most

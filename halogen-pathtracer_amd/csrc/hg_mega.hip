@@ -940,6 +940,15 @@ __shared__ SvWave hg_sv;
 __device__ __forceinline__ unsigned long long* sv_word64(const HgKernelParams& kp, uint32_t word) {
     return reinterpret_cast<unsigned long long*>(kp.queue + word);
 }
+// A control word read by a scalar load that bypasses the scalar cache (glc), from uncached memory (the runtime allocates
+// the control block so: no L2 holds it either).  The polling of idle waves stays off the CU's vector-memory pipe, whose
+// texture units return data in order: a vector poll of a contended coherent word held up the loads of the busy waves
+// beside it (with the idle waves of a frame's end polling, a posted frame took several times its trace time).
+__device__ __forceinline__ unsigned long long sv_sload(const unsigned long long* p) {
+    unsigned long long v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -982,8 +991,7 @@ __device__ __forceinline__ uint32_t sv_units(unsigned long long w) {
 // Refresh the view from the device mirror of the post word
 __device__ uint32_t sv_view(const HgKernelParams& kp) {
     uint32_t v = lds_get(hg_sv.view);
-    const unsigned long long m = __hip_atomic_load(
-        sv_word64(kp, HG_SV_MIRROR_WORD + 32u * (blockIdx.x % HG_SV_MIRRORS)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long m = sv_sload(sv_word64(kp, HG_SV_MIRROR_WORD + 32u * (blockIdx.x % HG_SV_MIRRORS)));
     const uint32_t u = sv_units(m);
     if (u > v) {
         v = u;
@@ -997,7 +1005,7 @@ __device__ uint32_t sv_view(const HgKernelParams& kp) {
 __device__ uint32_t sv_poll(const HgKernelParams& kp) {
     unsigned long long* const ticket = sv_word64(kp, HG_SV_TICKET_WORD + 32u * (blockIdx.x & 7u));
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    unsigned long long t = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long t = sv_sload(ticket);
     if (now >= t && __hip_atomic_compare_exchange_strong(ticket, &t, now + HG_SV_POLL_TICKS, __ATOMIC_RELAXED,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         const unsigned long long h = __hip_atomic_load(
@@ -1108,8 +1116,8 @@ __device__ uint32_t sv_wait(const HgKernelParams& kp) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t seen = HG_NONE;  // the view at which the heads were last read
     for (uint32_t spin = 0;; ++spin) {
-        // one coherent load per spin (this wave's mirror copy); the host word through the ticket every 4th spin
-        const uint32_t view = (spin & 3u) == 0u ? sv_poll(kp) : sv_view(kp);
+        // one coherent load per spin (this wave's mirror copy); the host word through the ticket every few spins
+        const uint32_t view = (spin % HG_SV_POLL_EVERY) == 0u ? sv_poll(kp) : sv_view(kp);
         const uint32_t pend = lds_get(hg_sv.pend);
         bool open = pend != HG_NONE && pend < view;
         if (!open && view != seen) {  // the heads, only when the posted units changed
@@ -1122,9 +1130,9 @@ __device__ uint32_t sv_wait(const HgKernelParams& kp) {
         }
         if (lds_get(hg_sv.stop)) return 1u;  // the final post word: nothing posted is left to claim
         if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(lds_get(hg_sv.idle_ticks))) return 1u;
-        // about 0.2 us between the first polls, then about 3.4 us (s_sleep counts 64 clocks)
-        if (spin < 16u) __builtin_amdgcn_s_sleep(8);
-        else __builtin_amdgcn_s_sleep(127);
+        // short sleeps between the first polls, then longer ones (s_sleep counts 64 clocks)
+        if (spin < HG_SV_SPIN_SHORT) __builtin_amdgcn_s_sleep(HG_SV_SLEEP_SHORT);
+        else __builtin_amdgcn_s_sleep(HG_SV_SLEEP_LONG);
     }
 }
 // (the colour stores of a server frame: fc_store into the uncached ring)
@@ -1490,11 +1498,15 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
 // (64-thread groups, no LDS, few registers).
 __global__ __launch_bounds__(64) void hg_server_gate(const uint32_t* __restrict__ done, uint32_t target,
                                                      uint64_t timeout_ticks, unsigned long long* __restrict__ err) {
-    if (threadIdx.x != 0) return;
+    // (the whole wave polls with scalar loads of the uncached count: nothing on the vector-memory pipe of the CU it
+    // shares with the server's waves; sv_sload)
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t spin = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+    for (uint32_t spin = 0;; ++spin) {
+        uint32_t n;
+        asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(n) : "s"(done) : "memory");
+        if (n >= target) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (threadIdx.x == 0) __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         if (spin < 256u) __builtin_amdgcn_s_sleep(1);

@@ -432,6 +432,8 @@ int hg_create(int device, hg_ctx** out) {
     hg_ctx* c = new hg_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->call_done[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->call_done[1], hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->counters_dev.p, 32 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return HG_E_HIP;
@@ -518,6 +520,8 @@ void hg_destroy(hg_ctx* c) {
     for (auto& pr : c->pending_trace) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : c->free_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (hipEvent_t e : c->call_done)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     sv_trace("destroy: done");
     delete c;
@@ -905,7 +909,9 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
             return HG_E_UNSUPPORTED;
         }
         for (hipEvent_t& e : S.blended) HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&S.host), 256, hipHostMallocMapped));
+        // coherent (fine-grained): the waves' system-scope loads of the post word must not hit a cached copy (with the
+        // default non-coherent pinned memory a post took milliseconds to reach idle waves)
+        HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&S.host), 256, hipHostMallocMapped | hipHostMallocCoherent));
         S.host[0] = S.host[1] = 0ull;
     }
     const uint32_t tiles = uint32_t(c->n_local_tiles);
@@ -931,7 +937,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
         HG_HIP(c, hipStreamSynchronize(c->stream));
     int rc = ensure_uncached(c, S.ring, size_t(ring) * per_frame);
     if (!rc) rc = ensure_uncached(c, S.done, size_t(ring) * 128u);
-    if (!rc) rc = ensure(c, S.ctl, HG_SV_CTL_BYTES);
+    if (!rc) rc = ensure_uncached(c, S.ctl, HG_SV_CTL_BYTES);  // (polled by scalar loads: hg_mega.hip sv_sload)
     if (!rc && spill_bytes) rc = ensure(c, S.spill, spill_bytes);
     if (!rc && c->tile_order_on) rc = ensure(c, S.tile_cost, 2 * tb);
     if (!rc && c->tile_order_on) rc = ensure(c, S.tile_order, tb);
@@ -1068,6 +1074,24 @@ int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
         }
     }
     return HG_OK;
+}
+
+// The host runs ahead of the GPU: the render call before the previous one has not finished on the device.  Only then
+// does the render server pay: it removes the drain at each frame's end, which a host that waits for every frame (a
+// display at once, or one frame behind) never sees behind its own wait, while the server's resident waves slow the
+// display's untile and copy beside them.
+bool host_ahead(hg_ctx* c) {
+    const int k = int(c->calls & 1u);  // recorded by the call before last
+    if (!c->call_done_valid[k]) return false;
+    const hipError_t q = hipEventQuery(c->call_done[k]);
+    (void)hipGetLastError();  // hipErrorNotReady is a status here
+    return q == hipErrorNotReady;
+}
+// After a render call's work is queued: its completion event, for host_ahead
+void note_call(hg_ctx* c) {
+    const int k = int(c->calls & 1u);
+    c->call_done_valid[k] = hipEventRecord(c->call_done[k], c->stream) == hipSuccess;
+    c->calls++;
 }
 
 // One launch of n_frames frames from FrameCount = params.frameCount (which it advances when accumulating)
@@ -1214,10 +1238,12 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
 
         c->counters.last_kernel = uint64_t(regen ? kern : HG_KERNEL_MEGA);
         // the reference's one frame per call: posted to the render server (persistent trace waves)
-        if (c->server_on && stream_k && pipelined && accumulate && n_frames <= HG_QUEUE_MAX_FRAMES && tiles > 0) {
+        if (c->server_on && stream_k && pipelined && accumulate && n_frames <= HG_QUEUE_MAX_FRAMES && tiles > 0 &&
+            (c->server_on == 2 || host_ahead(c))) {
             const int rc = server_render(c, kp, n_frames);
             if (rc == HG_OK) {
                 HG_HIP(c, hipEventRecord(ev.second, c->stream));
+                note_call(c);
                 c->pending.push_back(ev);
                 c->counters.launches++;
                 if (c->pending.size() + c->pending_trace.size() > 4096)
@@ -1397,6 +1423,7 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
         }
     }
     HG_HIP(c, hipEventRecord(ev.second, c->stream));
+    note_call(c);
     c->pending.push_back(ev);
     c->counters.launches++;
     if (c->pending.size() + c->pending_trace.size() > 4096) {
@@ -1816,7 +1843,8 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             c->lane_pick = value ? 1 : 0;
             return HG_OK;
         case HG_OPT_SERVER:
-            c->server_on = value ? 1 : 0;
+            if (value < 0 || value > 2) return fail(c, HG_E_INVALID, "HG_OPT_SERVER %d: expected 0, 1 or 2", value);
+            c->server_on = value;
             return HG_OK;
         case HG_OPT_WAVE_UNITS:
             if (value < 0 || value > HG_WAVE_UNITS_LIMIT)

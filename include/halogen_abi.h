@@ -239,7 +239,10 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
  *   frame's completion, in frame order, so every readback / gather sees exactly the frames rendered before it.  The
  *   server is stopped (its waves trace what was posted, then leave) by uploads, resize, tiling, options, counters,
  *   hg_synchronize, hg_destroy, a launch of another kind, or parameters / FrameCount that do not continue its chain.
- *   0 = every call launches (the round-4 per-launch pipeline).  Same images either way. */
+ *   1 (automatic) uses the server only while the host runs ahead of the GPU (the call before last still in flight on
+ *   the device: a host that queues frames); a host that waits for each frame (a display at once or one frame behind)
+ *   launches per call, which measured faster there.  2 = always (while the calls qualify).  0 = every call launches
+ *   (the round-4 per-launch pipeline).  Same images either way. */
 /* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
  *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
  *   device image and copied on the context stream.  Same images either way. */

@@ -1,4 +1,5 @@
-"""The render server (HG_OPT_SERVER, csrc/hg_mega.hip kServer), through the C-ABI.
+"""The render server (HG_OPT_SERVER, csrc/hg_mega.hip kServer), through the C-ABI.  The tests
+force it on (HG_OPT_SERVER 2: every qualifying call) except the one for the automatic choice (1, the default).
 
 The reference dispatches HalogenCompute once per frame (RP:327, RP:406).  hg_render calls of few accumulating frames on
 the streaming kernel post their frames to persistent trace waves that outlive the call; each frame's blend runs on the
@@ -20,7 +21,7 @@ from test_gpu_parity import assert_bitwise, gpu_render
 GOLD = Path(__file__).resolve().parent / "golden"
 
 
-def _ctx(packed, params, cube=None, server=1, coalesce=1, tiling=None):
+def _ctx(packed, params, cube=None, server=2, coalesce=1, tiling=None):
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)
     ctx = abi.Context(0)
     ctx.set_option(abi.HG_OPT_SERVER, server)
@@ -175,7 +176,7 @@ def test_gpu_server_restarts_keep_the_image(gpu):
             cnt = ctx.counters()
         return imgs, cnt
 
-    on, con = run(1)
+    on, con = run(2)
     off, coff = run(0)
     for k, (a, b) in enumerate(zip(on, off)):
         assert_bitwise(a, b, f"server restarts, readback {k}")
@@ -231,3 +232,29 @@ def test_gpu_server_full_size_c3_with_display(gpu):
     # (one restart allowed: the first display readback allocates its pinned host images, a gap that may exceed the
     # host's 20-ms restart threshold while no frame is in flight)
     assert cnt["server_launches"] <= 2 and cnt["server_frames"] == 64, cnt
+
+
+@pytest.mark.gpu
+def test_gpu_server_automatic_engages_only_ahead(gpu):
+    """HG_OPT_SERVER 1 (the default): a host that queues one-frame calls (C3 1080p, no readback between them) runs
+    ahead of the GPU and gets the server; a host that reads every frame back before the next call (the reference's
+    display) never runs ahead and launches per call.  Both images equal the batched launch bit for bit."""
+    cfg = scenes.CONFIGS["C3"]
+    packed, params, cube = _sized("C3", cfg.width, cfg.height)
+    W, H = cfg.width, cfg.height
+    want = gpu_render(packed, params, 24, True, cube)[0]
+    for display in (False, True):
+        ctx, _, _ = _ctx(packed, params, cube, server=1)
+        with ctx:
+            for _ in range(24):
+                ctx.render(1, True)
+                if display:
+                    ctx.readback_begin(abi.HG_DISPLAY_R11G11B10F)
+                    ctx.readback_end(W, H)
+            img = ctx.readback(W, H)
+            cnt = ctx.counters()
+        assert_bitwise(img, want, f"automatic server, display {display}")
+        if display:
+            assert cnt["server_launches"] == 0, cnt
+        else:
+            assert cnt["server_launches"] >= 1 and cnt["server_frames"] >= 16, cnt
