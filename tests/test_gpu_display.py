@@ -89,8 +89,8 @@ def test_gpu_display_format_tiling(gpu):
 def test_gpu_render_pass_display_latency_and_clear(gpu):
     """The Python HalogenRenderPass's display (as the C# and C++ passes): by default (latency 0, the reference's) each
     display() returns the frame just traced; with latency 1, the previous frame's image.  A camera move
-    (ClearAccumulation, RP:262-268) ends the readbacks in flight unseen and shows the first moved frame at once, so no
-    image from before the clear is ever shown."""
+    (ClearAccumulation, RP:262-268; the first frame's resolution setup is one too) ends the readbacks in flight unseen
+    and shows the first frame after it at once, so no image from before the clear is ever shown."""
     from halogen import render_pass as rp, scenes
     from halogen.unity import Transform
     cfg = scenes.CONFIGS["C1"].resized(40, 32, 4)
@@ -118,8 +118,10 @@ def test_gpu_render_pass_display_latency_and_clear(gpu):
     for c in views:
         p.Execute(scene, c)
         got.append(p.display())
-    assert got[0] is None  # the pipeline fills
-    for k in (1, 2, 3):
+    # the first frame follows a clear too (the first OnCameraSetup's): shown at once, then the pipeline fills
+    assert np.array_equal(got[0], want[0])
+    assert got[1] is None
+    for k in (2, 3):
         assert np.array_equal(got[k], want[k - 1]), k
     assert np.array_equal(got[4], want[4]), "the first frame after the camera move, shown at once"
     assert got[5] is None  # the pipeline refills behind it

@@ -139,10 +139,12 @@ def test_gpu_partial_reupload_sphere_count_and_cull_flip(gpu, name):
             ctx.set_params(params)
             ctx.render(2, True)
             if variant is packed:  # a round trip through both changes, back to the first arrays
-                ctx.upload_scene(singular)
-                ctx.render(1, True)
-                ctx.upload_scene(fewer)
-                ctx.render(1, True)
+                for step in (singular, fewer):
+                    ctx.upload_scene(step)
+                    sp = cases.setup(name)[1]
+                    sp.bufferCounts = abi.Vec4(len(step.spheres), len(step.meshes), 0.0, 0.0)
+                    ctx.set_params(sp)
+                    ctx.render(1, True)
             ctx.upload_scene(variant)
             ctx.clear_accumulation()
             ctx.set_params(vparams)
