@@ -19,8 +19,9 @@ def main():
     tag = sys.argv[1]
     src = ROOT / "gpurun_out" / "prof"
     out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --per-frame-only --steps 2 --coalesce {1,32} "
-                      "(C3, 2 x 64 hg_render(1) calls after one 64-frame warm-up)"}
-    for co in (1, 32):
+                      "[--server 0] (C3, 2 x 64 hg_render(1) calls after one 64-frame warm-up)"}
+    runs = [co for co in ("1", "1_srv0", "32") if (src / f"{tag}_perframe_co{co}").exists()]
+    for co in runs:
         d = src / f"{tag}_perframe_co{co}"
         stats = next(d.glob("*_kernel_stats.csv"))
         shutil.copy(stats, ROOT / "profiles" / f"{tag}_perframe_co{co}_kernel_stats.csv")
@@ -38,7 +39,7 @@ def main():
         bench = [json.loads(x) for x in open(src / f"{tag}_perframe_co{co}.log") if x.startswith('{"per_frame_only"')]
         out[f"coalesce_{co}"] = {"bench": bench[-1] if bench else None, "kernels": kernels}
     (ROOT / "profiles" / f"{tag}_perframe_summary.json").write_text(json.dumps(out, indent=1) + "\n")
-    for co in (1, 32):
+    for co in runs:
         print(co, out[f"coalesce_{co}"]["bench"])
 
 
