@@ -949,8 +949,17 @@ __device__ __forceinline__ unsigned long long sv_sload(const unsigned long long*
     asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
     return v;
 }
+// The same for a 32-bit word (a unit head); the address made wave-uniform (lane 0's branch: a value read from LDS
+// counts as divergent).  readfirstlane returns int: each half through uint32_t, or a low half >= 2^31 would
+// sign-extend over the high one.
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32)));
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(a)));
+    const uint32_t* const q = reinterpret_cast<const uint32_t*>((uint64_t(hi) << 32) | lo);
+    uint32_t v;
+    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
+    return v;
 }
 template <class T>
 __device__ __forceinline__ T* sv_ptr(uint32_t lo, uint32_t hi) {
