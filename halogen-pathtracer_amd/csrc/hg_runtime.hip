@@ -574,6 +574,10 @@ int hg_upload_scene_gen(hg_ctx* c, uint64_t geometry_generation, const HalogenSp
         if (same[0] && same[1] && same[2] && same[3] && same[4]) {
             c->scene_uploads_skipped++;
             c->scene_uploads_vouched += vouched ? 1u : 0u;
+            // (compared equal: the caller's generation now names the device's geometry, so the next upload under it is
+            // vouched for; without this, a first tagged upload of an untagged scene never let the next ones skip the
+            // compare)
+            c->geometry_gen = geometry_generation;
             return HG_OK;
         }
     }

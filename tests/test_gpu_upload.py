@@ -153,3 +153,45 @@ def test_gpu_partial_reupload_sphere_count_and_cull_flip(gpu, name):
             cnt = ctx.counters()
         assert cnt["scene_uploads_partial"] >= 1 and cnt["scene_uploads_skipped"] == 0, (what, cnt)
         assert_bitwise(img, want, f"{name}: partial re-upload, {what}")
+
+
+@pytest.mark.gpu
+def test_gpu_upload_generation_vouches_for_geometry(gpu):
+    """hg_upload_scene_gen: an upload under the generation of the last one skips the compare of the triangles and BVH
+    entries (hg_counters.scene_uploads_vouched) and only compares the small arrays.  A first tagged upload of an
+    untagged scene compares everything and adopts the generation; later ones under it are vouched for, an unchanged
+    scene skipped and a changed material rebuilt as a partial upload, both equal to a fresh upload's render; a new
+    generation compares everything again."""
+    packed, params, cube, frames, acc = cases.setup("dragon1_64x36")
+    W, H = int(params.screenParameters.x), int(params.screenParameters.y)
+    want, _ = gpu_render(packed, params, 4, True, cube)
+    changed = _copy(packed)
+    changed.materials[0].roughness = np.float32(0.3)
+    want_changed, _ = gpu_render(changed, params, 2, True, cube)
+    with abi.Context(0) as ctx:
+        ctx.upload_scene(packed)  # untagged
+        if cube is not None:
+            ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+        ctx.resize(W, H)
+        ctx.set_params(params)
+        ctx.render(2, True)
+        ctx.upload_scene(packed, generation=7)  # compared (generation new), equal: skipped, generation adopted
+        c0 = ctx.counters()
+        assert c0["scene_uploads_skipped"] == 1 and c0["scene_uploads_vouched"] == 0, c0
+        ctx.upload_scene(_copy(packed), generation=7)  # vouched: small arrays compared only
+        ctx.render(2, True)
+        img = ctx.readback(W, H)
+        c1 = ctx.counters()
+        assert c1["scene_uploads_skipped"] == 2 and c1["scene_uploads_vouched"] == 1, c1
+        assert_bitwise(img, want, "vouched re-upload")
+        ctx.upload_scene(changed, generation=7)  # a material changed: partial rebuild, still vouched
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+        ctx.render(2, True)
+        img = ctx.readback(W, H)
+        c2 = ctx.counters()
+        assert c2["scene_uploads_partial"] == 1 and c2["scene_uploads_vouched"] == 2, c2
+        assert_bitwise(img, want_changed, "vouched partial re-upload")
+        ctx.upload_scene(changed, generation=8)  # a new generation: compared again (equal: skipped, not vouched)
+        c3 = ctx.counters()
+        assert c3["scene_uploads_skipped"] == 3 and c3["scene_uploads_vouched"] == 2, c3
