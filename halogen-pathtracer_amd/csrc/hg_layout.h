@@ -157,9 +157,6 @@
 #define HG_SV_SPIN_SHORT 16u
 #define HG_SV_POLL_EVERY 4u  // an idle wave reads the host word (if its XCD's ticket is free) every this many spins
 #endif
-#ifndef HG_SV_RESERVE
-#define HG_SV_RESERVE 4u  // units a server wave claims per head atomic (handed out one by one from its LDS)
-#endif
 #ifndef HG_SV_WAVES
 #define HG_SV_WAVES 5  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
 #endif

@@ -929,8 +929,7 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
 struct SvWave {
     uint32_t view;   // units posted as this wave last saw them
     uint32_t dry;    // the view at which this wave last found every head dry (HG_NONE: none)
-    uint32_t pend;   // a claimed unit whose frame window was busy (HG_NONE: none; claims never pass the posted units)
-    uint32_t res_next, res_left;  // units claimed ahead from one head (HG_SV_RESERVE per atomic): the next, how many
+    uint32_t pend;   // a unit claimed beyond the view, or whose frame window was busy (HG_NONE: none)
     uint32_t stop;   // the stop flag as this wave last saw it
     uint32_t nlt, mask, cap, magic, shift, idle_ticks;  // tiles per frame, ring slots - 1, frames cap, u / nlt, leave after
     uint32_t post_lo, post_hi, done_lo, done_hi;        // the host post word and the ring-slot counts (pointers)
@@ -970,8 +969,6 @@ __device__ void sv_init(const HgKernelParams& kp) {  // lane 0, at the kernel's 
     lds_put(hg_sv.view, 0u);
     lds_put(hg_sv.dry, HG_NONE);
     lds_put(hg_sv.pend, HG_NONE);
-    lds_put(hg_sv.res_next, 0u);
-    lds_put(hg_sv.res_left, 0u);
     lds_put(hg_sv.stop, 0u);
     lds_put(hg_sv.nlt, uint32_t(kp.n_local_tiles));
     lds_put(hg_sv.mask, kp.sv_ring - 1u);
@@ -1036,46 +1033,26 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
     lds_put(q.end, base);
     uint32_t u = lds_get(hg_sv.pend);
     uint32_t view = lds_get(hg_sv.view);
-    if (u == HG_NONE && lds_get(hg_sv.res_left) != 0u) {  // the next unit claimed ahead
-        u = lds_get(hg_sv.res_next);
-        lds_put(hg_sv.res_next, u + 8u);
-        lds_put(hg_sv.res_left, lds_get(hg_sv.res_left) - 1u);
-    } else if (u == HG_NONE) {
+    if (u == HG_NONE) {
         if (view == lds_get(hg_sv.dry)) {  // every head was dry at this view: anything new posted?  (A busy wave
             view = sv_poll(kp);            // polls the host word too: no wave may be waiting to do it)
             if (view == lds_get(hg_sv.dry)) return;
         }
-        // Up to HG_SV_RESERVE posted units per claim (each atomic of uncached memory is a long load in the CU's
-        // in-order texture pipe: the loads of the busy waves behind it wait for its return), claimed by a
-        // compare-and-swap that never takes a unit beyond the posted ones: a claimed unit is always traceable now,
-        // so no wave can sit on a unit that is not posted while posted ones wait (one wave per tile, a single-tile
-        // image: the server's only wave must reach every head's units)
         const uint32_t x = blockIdx.x & 7u;
         for (uint32_t t = 0; t < 8u && u == HG_NONE; ++t) {  // own XCD's head first, then steal
             const uint32_t h = (x + t) & 7u;
-            uint32_t* const head = kp.queue + 32u * h;
-            uint32_t v = ld_agent(head);
-            for (uint32_t attempt = 0; attempt < 4u; ++attempt) {
-                const uint32_t lim = view > h ? (view - h + 7u) >> 3 : 0u;  // units h + 8 n < view: n < lim
-                if (v >= lim) break;
-                const uint32_t r = min(lim - v, HG_SV_RESERVE);
-                if (__hip_atomic_compare_exchange_strong(head, &v, v + r, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) {
-                    u = h + 8u * v;
-                    lds_put(hg_sv.res_next, u + 8u);
-                    lds_put(hg_sv.res_left, r - 1u);
-                    break;
-                }  // (v now holds the head's current value)
-            }
+            if (h + 8u * ld_agent(kp.queue + 32u * h) >= view) continue;
+            u = h + 8u * atomicAdd(kp.queue + 32u * h, 1u);
         }
         if (u == HG_NONE) {
             lds_put(hg_sv.dry, view);
             return;
         }
     }
+    if (u >= view) view = sv_view(kp);
     const uint32_t k = sv_frame(u), w = k & 3u;
-    if (lds_get(hg_sv.win_units[w]) != 0u && lds_get(hg_sv.win_frame[w]) != k) {
-        lds_put(hg_sv.pend, u);  // its frame window still busy (the wave's own items of frame k - 4j): later
+    if (u >= view || (lds_get(hg_sv.win_units[w]) != 0u && lds_get(hg_sv.win_frame[w]) != k)) {
+        lds_put(hg_sv.pend, u);  // (claimed past the posted frames by a race, or its frame window still busy): later
         return;
     }
     lds_put(hg_sv.pend, HG_NONE);
@@ -1150,8 +1127,13 @@ __device__ uint32_t sv_wait(const HgKernelParams& kp) {
     for (uint32_t spin = 0;; ++spin) {
         // one coherent load per spin (this wave's mirror copy); the host word through the ticket every few spins
         const uint32_t view = (spin % HG_SV_POLL_EVERY) == 0u ? sv_poll(kp) : sv_view(kp);
-        bool open = lds_get(hg_sv.pend) != HG_NONE || lds_get(hg_sv.res_left) != 0u;  // (both always posted)
-        if (!open && view != seen) {  // the heads, only when the posted units changed
+        // A wave holding a unit (claimed past the posted ones by a race with another claimer, or with its frame
+        // window busy) claims nothing else until it is placed: it waits for that unit alone.  (No wave set can end
+        // up all holding unposted units while posted ones remain: the last claimer's overshoot needs a concurrent
+        // claimer, which then holds none.)
+        const uint32_t pend = lds_get(hg_sv.pend);
+        bool open = pend != HG_NONE && pend < view;
+        if (pend == HG_NONE && view != seen) {  // the heads, only when the posted units changed
             seen = view;
             for (uint32_t h = 0; h < 8u && !open; ++h) open = h + 8u * ld_agent(kp.queue + 32u * h) < view;
         }
