@@ -1,10 +1,10 @@
 #!/bin/bash
-# The whole -m gpu suite (server tests first), one process, progress per test in gpurun_out/suite/
+# The whole -m gpu suite (server tests first), one process per step, progress per test in gpurun_out/suite/
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/suite
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_server.py -x -v --timeout 240 --timeout-method thread > $O/server.log 2>&1 || { echo "server tests failed"; tail -30 $O/server.log; exit 1; }
-tail -2 $O/server.log
+tail -1 $O/server.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread --deselect tests/test_gpu_server.py > $O/all.log 2>&1; rc=$?
-tail -3 $O/all.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/all.log | head -20; exit $rc; }
+tail -2 $O/all.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/all.log | head -20; exit $rc; }
