@@ -229,9 +229,9 @@ def test_gpu_server_full_size_c3_with_display(gpu):
     assert_bitwise(img, want[64], "C3 1080p, 64 frames through the server")
     for k in checks:
         assert np.array_equal(shown[k - 1], abi.pack_display(want[k], abi.HG_DISPLAY_R11G11B10F)), f"displayed frame {k}"
-    # (one restart allowed: the first display readback allocates its pinned host images, a gap that may exceed the
-    # host's 20-ms restart threshold while no frame is in flight)
-    assert cnt["server_launches"] <= 2 and cnt["server_frames"] == 64, cnt
+    # (a few restarts allowed: the first display readbacks allocate their pinned host images, gaps that may exceed the
+    # host's 20-ms restart threshold while no frame is in flight; every frame still went through the server)
+    assert cnt["server_launches"] <= 4 and cnt["server_frames"] == 64, cnt
 
 
 @pytest.mark.gpu
