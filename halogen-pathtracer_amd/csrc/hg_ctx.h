@@ -87,7 +87,6 @@ struct hg_ctx {
         DevBuf done;        // per ring slot a completion count on its own 128-B line, zeroed before each launch
         DevBuf ring;        // colour ring: ring_n frames of n_local_tiles * 64 float4
         DevBuf spill, tile_cost, tile_order, order_scratch;
-        std::vector<uint32_t> band_order;  // (HALOGEN_SERVER_BANDS experiment) the host copy of a banded order
         bool tile_cost_valid = false;
         unsigned long long* host = nullptr;  // pinned: [0] the post word (frames | stop << 32), [1] a gate's timeout
         uint32_t ring_n = 0, posted = 0, cap = 0;

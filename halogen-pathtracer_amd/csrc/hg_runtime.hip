@@ -976,18 +976,6 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
             S.tile_cost_valid = true;
         }
     }
-    // (experiment, HALOGEN_SERVER_BANDS=1: head h's units, positions h + 8 j of each frame, are the j-th tile of the
-    // image's h-th horizontal band, so each XCD, which pulls from its own head first, traces one band: L2 locality)
-    static const bool bands = std::getenv("HALOGEN_SERVER_BANDS") != nullptr;
-    if (bands && tiles % 8u == 0u && S.tile_order.p) {
-        S.band_order.resize(tiles);
-        const uint32_t per = tiles / 8u;
-        for (uint32_t j = 0; j < per; ++j)
-            for (uint32_t h = 0; h < 8u; ++h) S.band_order[h + 8u * j] = h * per + j;
-        HG_HIP(c, hipMemcpyAsync(S.tile_order.p, S.band_order.data(), size_t(tiles) * 4u, hipMemcpyHostToDevice,
-                                 S.stream));
-        kp.tile_order = static_cast<const uint32_t*>(S.tile_order.p);
-    }
     kp.frame_color = static_cast<float4*>(S.ring.p);
     kp.frames_done = static_cast<uint32_t*>(S.done.p);
     kp.queue = static_cast<uint32_t*>(S.ctl.p);
