@@ -160,6 +160,9 @@
 #ifndef HG_SV_WAVES
 #define HG_SV_WAVES 5  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
 #endif
+#ifndef HG_SV_DIAG_NO_BLEND
+#define HG_SV_DIAG_NO_BLEND 0  // analysis builds: the render server's frames are gated but never blended
+#endif
 #ifndef HG_SV_RING
 #define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most
 #endif

@@ -1541,7 +1541,7 @@ hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_
                                   const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
                                   unsigned long long* err, hipStream_t stream) {
     hipLaunchKernelGGL(hg_server_gate, dim3(1), dim3(64), 0, stream, done, target, timeout_ticks, err);
-    if (n_slots)
+    if (n_slots && !HG_SV_DIAG_NO_BLEND)  // (analysis builds only: no blend, to price it; the image is wrong)
         hipLaunchKernelGGL(hg_server_blend, dim3((n_slots + 63) / 64), dim3(64), 0, stream, acc, colors, n_slots,
                            frame_count);
     return hipGetLastError();
