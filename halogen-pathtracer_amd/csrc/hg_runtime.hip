@@ -913,8 +913,9 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
             return HG_E_UNSUPPORTED;
         }
         for (hipEvent_t& e : S.blended) HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        // coherent (fine-grained): the waves' system-scope loads of the post word must not hit a cached copy (with the
-        // default non-coherent pinned memory a post took milliseconds to reach idle waves)
+        // coherent (fine-grained) pinned memory: the pollers' system-scope loads of the post word read host memory
+        // itself (measured the same as the default pinned memory, tools/sweeps/sweep_r05_server.txt; this is the
+        // memory type whose coherence the loads rely on)
         HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&S.host), 256, hipHostMallocMapped | hipHostMallocCoherent));
         S.host[0] = S.host[1] = 0ull;
     }
