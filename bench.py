@@ -169,7 +169,8 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     accumulator) is rendered as `frames` x hg_render(1) and compared bit for bit with one hg_render(frames), then timed
     (`reps` steps; device sync on both sides):
       value       the library's default: consecutive calls are held and launched HG_OPT_COALESCE (32) frames at a time;
-      strict      HG_OPT_COALESCE 1: every call its own launch (traces of consecutive launches overlap on two streams);
+      strict      HG_OPT_COALESCE 1: every call its own; the render server serves them once the host runs ahead
+                  (HG_OPT_SERVER 1), and `strict.per_launch` times the same calls with a launch each (HG_OPT_SERVER 0);
       with_readback  hg_readback of the 33 MB image into a caller buffer after every call (which launches the held
                   frame, so this is one launch per frame too);
       with_display_readback  the C# pass's per-frame display path, hg_readback_begin/_end into the context's pinned
@@ -183,6 +184,7 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     def timed(coalesce: int):
         ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
         ctx.reset_counters()
+        before = ctx.counters()  # (the server's counts run since hg_create: their difference is this run's)
         fresh()
         ctx.synchronize()
         t0 = time.perf_counter()
@@ -192,21 +194,29 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         ctx.synchronize()
         dt = time.perf_counter() - t0
         c = ctx.counters()
+        for k in ("server_launches", "server_frames"):
+            c[k] = c.get(k, 0) - before.get(k, 0)
         return dt, c
 
     fresh()
     ctx.render(frames, True)
     batched = ctx.readback(W, H)
     identical = {}
-    for coalesce in (1, 32):
+    for coalesce, server in ((1, 1), (32, 1), (1, 2), (1, 0)):
         ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
+        ctx.set_option(abi.HG_OPT_SERVER, server)
         fresh()
         for _ in range(frames):
             ctx.render(1, True)
-        identical[f"coalesce_{coalesce}"] = bool(np.array_equal(batched.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
+        key = f"coalesce_{coalesce}" + {1: "", 2: "_server", 0: "_no_server"}[server]
+        identical[key] = bool(np.array_equal(batched.view(np.uint32), ctx.readback(W, H).view(np.uint32)))
+    ctx.set_option(abi.HG_OPT_SERVER, 1)
     paths = W * H * frames
     dt, c = timed(32)
-    dt_s, c_s = timed(1)
+    dt_s, c_s = timed(1)  # (the render server engages once the host runs ahead: HG_OPT_SERVER 1, the default)
+    ctx.set_option(abi.HG_OPT_SERVER, 0)  # the same calls, a launch per call (round 4's pipeline), for comparison
+    dt_s0, c_s0 = timed(1)
+    ctx.set_option(abi.HG_OPT_SERVER, 1)
     img = np.empty((H, W, 4), np.float32)
     fresh()
     ctx.synchronize()
@@ -265,7 +275,11 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
             "unit": "Mpaths/s", "steps": reps, "ms_per_frame": dt * 1e3 / (reps * frames),
             "launches_per_step": c["launches"] / reps, "frac_of_batched": value / batched_value,
             "strict": {"value": strict, "ms_per_frame": dt_s * 1e3 / (reps * frames),
-                       "launches_per_step": c_s["launches"] / reps, "frac_of_batched": strict / batched_value},
+                       "launches_per_step": c_s["launches"] / reps, "frac_of_batched": strict / batched_value,
+                       "server_launches": c_s.get("server_launches", 0), "server_frames": c_s.get("server_frames", 0),
+                       "per_launch": {"value": paths * reps / dt_s0 / 1e6, "ms_per_frame": dt_s0 * 1e3 / (reps * frames),
+                                      "frac_of_batched": paths * reps / dt_s0 / 1e6 / batched_value,
+                                      "note": "HG_OPT_SERVER 0: every call its own launch"}},
             "with_readback": {"value": paths / dt_rb / 1e6, "unit": "Mpaths/s", "ms_per_frame": dt_rb * 1e3 / frames,
                               "readback_bytes_per_frame": W * H * 16},
             "with_display_readback": display,

@@ -88,7 +88,8 @@ def test_committed_bench_line_keeps_the_contract():
     cpu = line["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
     assert line["counting_replay_bit_identical"] is True
-    assert line["per_frame"]["bit_identical_to_batched"] == {"coalesce_1": True, "coalesce_32": True}
+    ident = line["per_frame"]["bit_identical_to_batched"]
+    assert {"coalesce_1", "coalesce_32"} <= set(ident) and all(ident.values()), ident
     fast = line["fast_bvh"]
     assert fast["value"] > line["value"] and fast["pixels_differing_from_headline_image"] < 1e-3
     fr = fast["roofline"]
