@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r05p2
 mkdir -p $O
-for v in shipped b16 b64; do
+for v in shipped; do
   if [ $v = shipped ]; then unset HALOGEN_LIB; else export HALOGEN_LIB=$PWD/halogen-pathtracer_amd/variants/$v/libhalogen_hip.so; fi
   timeout -k 10 120 python -u bench.py --per-frame-only --steps 4 --server 2 --display pipelined --display-format r11g11b10f --readback-depth 2 > $O/d2_$v.json 2> $O/d2_$v.err || { tail -3 $O/d2_$v.err; exit 1; }
   echo "$v one-behind $(cut -c1-110 $O/d2_$v.json)"
