@@ -97,6 +97,9 @@ struct hg_ctx {
         int32_t kernel_variant = 0, descent_t = 0;
         HgKernelParams kp{};  // the launch's parameters (the blends read acc / ring / first_frame)
         double last_post_s = 0.0;  // host clock of the last post
+#if HG_SV_DIAG_TIMES
+        double post_s[256] = {};  // (analysis builds) host clock of each post
+#endif
     } sv;
     int32_t server_on = 1;  // HG_OPT_SERVER
     uint64_t server_launches = 0, server_frames = 0;

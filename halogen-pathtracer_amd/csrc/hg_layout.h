@@ -147,7 +147,11 @@
 #define HG_SV_MIRROR_WORD 288u
 #define HG_SV_TICKET_WORD (HG_SV_MIRROR_WORD + 32u * HG_SV_MIRRORS)
 #define HG_SV_EXIT_WORD (HG_SV_TICKET_WORD + 32u * 8u)  // waves of the server that left | grid << 32
-#define HG_SV_CTL_BYTES ((HG_SV_EXIT_WORD + 32u) * 4u)
+#ifndef HG_SV_DIAG_TIMES
+#define HG_SV_DIAG_TIMES 0  // analysis builds: per frame (< 256) the device time of its first claim and its last count
+#endif
+#define HG_SV_DIAG_WORD (HG_SV_EXIT_WORD + 32u)
+#define HG_SV_CTL_BYTES ((HG_SV_DIAG_WORD + (HG_SV_DIAG_TIMES ? 1024u : 0u)) * 4u)
 #ifndef HG_SV_POLL_TICKS
 #define HG_SV_POLL_TICKS 200u  // 2 us between reads of the host word over PCIe, per XCD
 #endif

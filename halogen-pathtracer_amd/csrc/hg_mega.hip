@@ -1056,6 +1056,11 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
         return;
     }
     lds_put(hg_sv.pend, HG_NONE);
+#if HG_SV_DIAG_TIMES
+    if (k < 256u)  // (analysis builds) the frame's first claim: max of the complement
+        __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * k), ~(unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     const int tile = ordered_tile(kp, u - k * lds_get(hg_sv.nlt));
     const uint32_t g = uint32_t(kp.rank) + uint32_t(tile) * uint32_t(kp.n_ranks);
     const uint32_t ty = g / uint32_t(kp.tiles_x);
@@ -1081,7 +1086,8 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
 }
 // Frames of the window whose pulled items the lanes have all finished: after a drain of the wave's colour stores, their
 // units go to the frame's ring-slot count
-__device__ void sv_flush() {
+__device__ void sv_flush(const HgKernelParams& kp) {
+    (void)kp;
     bool drained = false;
     for (uint32_t w = 0; w < 4u; ++w) {
         const uint32_t n = lds_get(hg_sv.win_units[w]);
@@ -1095,6 +1101,12 @@ __device__ void sv_flush() {
         uint32_t* const done = sv_ptr<uint32_t>(lds_get(hg_sv.done_lo), lds_get(hg_sv.done_hi));
         __hip_atomic_fetch_add(done + 32u * (lds_get(hg_sv.win_frame[w]) & lds_get(hg_sv.mask)), n, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+#if HG_SV_DIAG_TIMES
+        if (lds_get(hg_sv.win_frame[w]) < 256u)  // (analysis builds) the frame's last count
+            __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * lds_get(hg_sv.win_frame[w]) + 2u),
+                                   (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#endif
         lds_put(hg_sv.win_units[w], 0u);
         lds_put(hg_sv.win_items[w], 0u);
         lds_put(hg_sv.win_done[w], 0u);
@@ -1103,7 +1115,7 @@ __device__ void sv_flush() {
 // Loop top: flush finished frames, keep both units filled (the spent one refilled after the other; both spent: two
 // new units, in turn).  Returns true when the wave has no item to hand out now.
 __device__ bool sv_refill(const HgKernelParams& kp) {
-    sv_flush();
+    sv_flush(kp);
     const uint32_t cnt = lds_get(hg_next_item);
     uint32_t a = lds_get(hg_q_cur);
     if (cnt >= lds_get(hg_qu[a].end)) {  // the first unit is spent

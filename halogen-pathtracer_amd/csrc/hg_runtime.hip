@@ -355,6 +355,19 @@ int server_stop(hg_ctx* c) {
     (void)hipGetLastError();  // hipErrorNotReady is a status here
     S.running = false;
     sv_trace("stopped after %.3f ms (%s)", (host_seconds() - t0) * 1e3, hipGetErrorString(q));
+#if HG_SV_DIAG_TIMES
+    {  // (analysis builds) per frame: first claim and last count on the device clock (10 ns), host post time
+        std::vector<unsigned long long> d(512);
+        if (hipMemcpy(d.data(), static_cast<char*>(S.ctl.p) + HG_SV_DIAG_WORD * 4u, d.size() * 8u,
+                      hipMemcpyDeviceToHost) == hipSuccess) {
+            const unsigned long long t00 = ~d[0];
+            for (uint32_t k = 0; k < std::min<uint32_t>(S.posted, 256u); ++k)
+                sv_trace("frame %u: posted %+.3f ms (host), first claim %+.3f ms, last count %+.3f ms (device)", k,
+                         (S.post_s[k] - S.post_s[0]) * 1e3, double(~d[2 * k] - t00) * 1e-5,
+                         double(d[2 * k + 1] - t00) * 1e-5);
+        }
+    }
+#endif
     if (q != hipSuccess) return fail(c, HG_E_HIP, "render server: %s", hipGetErrorString(q));
     return server_check(c);
 }
@@ -1050,6 +1063,9 @@ int server_post(hg_ctx* c) {
     S.blend_valid[s] = true;
     S.posted = k + 1u;
     __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted), __ATOMIC_SEQ_CST);
+#if HG_SV_DIAG_TIMES
+    if (k < 256u) S.post_s[k] = host_seconds();
+#endif
     S.last_post_s = host_seconds();
     c->server_frames++;
     sv_trace("posted %u (slot %u, target %u)", k, s, S.uses[s] * tiles);
