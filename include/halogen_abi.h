@@ -276,7 +276,9 @@ int hg_upload_scene(hg_ctx* ctx,
  * RayTracingManager's mesh list in the reference — changes), so they are not compared; the spheres, mesh records and
  * materials are compared as always (the reference re-reads transforms and materials on every re-upload, RP:448-509).
  * The reference re-uploads every buffer on each camera move (RP:262-268, 296-299): this keeps that call pattern at the
- * cost of the small arrays only.  Generation 0 (and every generation change) compares everything, as hg_upload_scene. */
+ * cost of the small arrays only.  Generation 0 (and every generation change) compares everything, as hg_upload_scene;
+ * an upload that compared everything adopts its generation for the next ones.  The vouch is trusted: triangles or BVH
+ * entries changed in place under an unchanged generation (same counts) keep the device's previous geometry. */
 int hg_upload_scene_gen(hg_ctx* ctx, uint64_t geometry_generation,
                         const HalogenSphere* spheres, int32_t n_spheres,
                         const HalogenMeshData* meshes, int32_t n_meshes,
