@@ -164,6 +164,9 @@
 #ifndef HG_SV_WAVES
 #define HG_SV_WAVES 5  // the render server's persistent waves per SIMD (hg_runtime.hip server_start)
 #endif
+#ifndef HG_SV_CLAIM
+#define HG_SV_CLAIM 4u  // units per claim of a server wave far behind the posted units (the rest held for its next pulls)
+#endif
 #ifndef HG_SV_DIAG_NO_BLEND
 #define HG_SV_DIAG_NO_BLEND 0  // analysis builds: the render server's frames are gated but never blended
 #endif

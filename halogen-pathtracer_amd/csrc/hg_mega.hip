@@ -930,6 +930,7 @@ struct SvWave {
     uint32_t view;   // units posted as this wave last saw them
     uint32_t dry;    // the view at which this wave last found every head dry (HG_NONE: none)
     uint32_t pend;   // a unit claimed beyond the view, or whose frame window was busy (HG_NONE: none)
+    uint32_t more, more_n;  // the rest of a multi-unit claim: more_n units from `more` in steps of 8, after pend
     uint32_t stop;   // the stop flag as this wave last saw it
     uint32_t nlt, mask, cap, magic, shift, idle_ticks;  // tiles per frame, ring slots - 1, frames cap, u / nlt, leave after
     uint32_t post_lo, post_hi, done_lo, done_hi;        // the host post word and the ring-slot counts (pointers)
@@ -969,6 +970,7 @@ __device__ void sv_init(const HgKernelParams& kp) {  // lane 0, at the kernel's 
     lds_put(hg_sv.view, 0u);
     lds_put(hg_sv.dry, HG_NONE);
     lds_put(hg_sv.pend, HG_NONE);
+    lds_put(hg_sv.more_n, 0u);
     lds_put(hg_sv.stop, 0u);
     lds_put(hg_sv.nlt, uint32_t(kp.n_local_tiles));
     lds_put(hg_sv.mask, kp.sv_ring - 1u);
@@ -1039,15 +1041,24 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
             if (view == lds_get(hg_sv.dry)) return;
         }
         const uint32_t x = blockIdx.x & 7u;
+        uint32_t take = 1u;
         for (uint32_t t = 0; t < 8u && u == HG_NONE; ++t) {  // own XCD's head first, then steal
             const uint32_t h = (x + t) & 7u;
-            if (h + 8u * ld_agent(kp.queue + 32u * h) >= view) continue;
-            u = h + 8u * atomicAdd(kp.queue + 32u * h, 1u);
+            const uint32_t n = ld_agent(kp.queue + 32u * h);
+            if (h + 8u * n >= view) continue;
+#if HG_SV_CLAIM > 1
+            // HG_SV_CLAIM units per atomic while the head holds posted units for as many claims of every wave of its
+            // XCD (one wave per block): no frame's end is left to a wave holding several
+            take = h + 8u * (n + HG_SV_CLAIM * (1u + gridDim.x / 8u)) < view ? HG_SV_CLAIM : 1u;
+#endif
+            u = h + 8u * atomicAdd(kp.queue + 32u * h, take);
         }
         if (u == HG_NONE) {
             lds_put(hg_sv.dry, view);
             return;
         }
+        lds_put(hg_sv.more, u + 8u);  // (placed after u)
+        lds_put(hg_sv.more_n, take - 1u);
     }
     if (u >= view) view = sv_view(kp);
     const uint32_t k = sv_frame(u), w = k & 3u;
@@ -1055,7 +1066,12 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
         lds_put(hg_sv.pend, u);  // (claimed past the posted frames by a race, or its frame window still busy): later
         return;
     }
-    lds_put(hg_sv.pend, HG_NONE);
+    const uint32_t more_n = lds_get(hg_sv.more_n);  // the next unit of a multi-unit claim, if any, is pulled next
+    lds_put(hg_sv.pend, more_n ? lds_get(hg_sv.more) : HG_NONE);
+    if (more_n) {
+        lds_put(hg_sv.more, lds_get(hg_sv.more) + 8u);
+        lds_put(hg_sv.more_n, more_n - 1u);
+    }
 #if HG_SV_DIAG_TIMES
     if (k < 256u)  // (analysis builds) the frame's first claim: max of the complement
         __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * k), ~(unsigned long long)__builtin_amdgcn_s_memrealtime(),
