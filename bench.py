@@ -167,7 +167,7 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
     """The drop-in's operating point: the reference dispatches HalogenCompute once per frame (RP:327, RP:406) and the
     C# shim calls hg_render(ctx, 1, 1) per Execute.  The same C3 step (`frames` progressive frames from a cleared
     accumulator) is rendered as `frames` x hg_render(1) and compared bit for bit with one hg_render(frames), then timed
-    (`reps` steps; device sync on both sides):
+    (`reps` steps, the headline's K: as many frames from one clear as its timed region; device sync on both sides):
       value       the library's default: consecutive calls are held and launched HG_OPT_COALESCE (32) frames at a time;
       strict      HG_OPT_COALESCE 1: every call its own; the render server serves them once the host runs ahead
                   (HG_OPT_SERVER 1), and `strict.per_launch` times the same calls with a launch each (HG_OPT_SERVER 0);
@@ -1052,7 +1052,7 @@ def main():
                 else timed_img
             np.save(args.save_image, img)
         if world == 1 and not emu and not args.no_per_frame:
-            result["per_frame"] = per_frame_measurement(ctx, params, W, H, frames_per_step, max(2, args.steps // 4),
+            result["per_frame"] = per_frame_measurement(ctx, params, W, H, frames_per_step, max(2, args.steps),
                                                         result["value"])
         if world == 1 and not emu and not args.no_per_frame:
             result["camera_move"] = camera_move_measurement(ctx, packed, s, cfg, W, H, 32, cube)
