@@ -167,12 +167,6 @@
 #ifndef HG_SV_CLAIM
 #define HG_SV_CLAIM 4u  // units per claim of a server wave far behind the posted units (the rest held for its next pulls)
 #endif
-#ifndef HG_SV_DIAG_CACHED_RING
-#define HG_SV_DIAG_CACHED_RING 0  // analysis builds: the server's colour ring in cached memory (the gate and blend may read
-#endif                            // stale lines: wrong images; prices the uncached ring's stores)
-#ifndef HG_SV_DIAG_NO_BLEND
-#define HG_SV_DIAG_NO_BLEND 0  // analysis builds: the render server's frames are gated but never blended
-#endif
 #ifndef HG_SV_RING
 #define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most
 #endif

@@ -1046,11 +1046,9 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
             const uint32_t h = (x + t) & 7u;
             const uint32_t n = ld_agent(kp.queue + 32u * h);
             if (h + 8u * n >= view) continue;
-#if HG_SV_CLAIM > 1
             // HG_SV_CLAIM units per atomic while the head holds posted units for as many claims of every wave of its
             // XCD (one wave per block): no frame's end is left to a wave holding several
-            take = h + 8u * (n + HG_SV_CLAIM * (1u + gridDim.x / 8u)) < view ? HG_SV_CLAIM : 1u;
-#endif
+            if (HG_SV_CLAIM > 1u) take = h + 8u * (n + HG_SV_CLAIM * (1u + gridDim.x / 8u)) < view ? HG_SV_CLAIM : 1u;
             u = h + 8u * atomicAdd(kp.queue + 32u * h, take);
         }
         if (u == HG_NONE) {
@@ -1072,11 +1070,9 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
         lds_put(hg_sv.more, lds_get(hg_sv.more) + 8u);
         lds_put(hg_sv.more_n, more_n - 1u);
     }
-#if HG_SV_DIAG_TIMES
-    if (k < 256u)  // (analysis builds) the frame's first claim: max of the complement
+    if (HG_SV_DIAG_TIMES && k < 256u)  // (analysis builds) the frame's first claim: max of the complement
         __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * k), ~(unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     const int tile = ordered_tile(kp, u - k * lds_get(hg_sv.nlt));
     const uint32_t g = uint32_t(kp.rank) + uint32_t(tile) * uint32_t(kp.n_ranks);
     const uint32_t ty = g / uint32_t(kp.tiles_x);
@@ -1117,12 +1113,10 @@ __device__ void sv_flush(const HgKernelParams& kp) {
         uint32_t* const done = sv_ptr<uint32_t>(lds_get(hg_sv.done_lo), lds_get(hg_sv.done_hi));
         __hip_atomic_fetch_add(done + 32u * (lds_get(hg_sv.win_frame[w]) & lds_get(hg_sv.mask)), n, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-#if HG_SV_DIAG_TIMES
-        if (lds_get(hg_sv.win_frame[w]) < 256u)  // (analysis builds) the frame's last count
+        if (HG_SV_DIAG_TIMES && lds_get(hg_sv.win_frame[w]) < 256u)  // (analysis builds) the frame's last count
             __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * lds_get(hg_sv.win_frame[w]) + 2u),
                                    (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-#endif
         lds_put(hg_sv.win_units[w], 0u);
         lds_put(hg_sv.win_items[w], 0u);
         lds_put(hg_sv.win_done[w], 0u);
@@ -1569,7 +1563,7 @@ hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_
                                   const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
                                   unsigned long long* err, hipStream_t stream) {
     hipLaunchKernelGGL(hg_server_gate, dim3(1), dim3(64), 0, stream, done, target, timeout_ticks, err);
-    if (n_slots && !HG_SV_DIAG_NO_BLEND)  // (analysis builds only: no blend, to price it; the image is wrong)
+    if (n_slots)
         hipLaunchKernelGGL(hg_server_blend, dim3((n_slots + 63) / 64), dim3(64), 0, stream, acc, colors, n_slots,
                            frame_count);
     return hipGetLastError();

@@ -953,11 +953,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     // them (an event, no host wait) unless a buffer must move (then the context stream is drained first)
     if (S.ring.bytes < size_t(ring) * per_frame || S.done.bytes < size_t(ring) * 128u)
         HG_HIP(c, hipStreamSynchronize(c->stream));
-#if HG_SV_DIAG_CACHED_RING  // (analysis builds: what the uncached ring's scattered 16-B stores cost; images wrong)
-    int rc = ensure(c, S.ring, size_t(ring) * per_frame);
-#else
     int rc = ensure_uncached(c, S.ring, size_t(ring) * per_frame);
-#endif
     if (!rc) rc = ensure_uncached(c, S.done, size_t(ring) * 128u);
     if (!rc) rc = ensure_uncached(c, S.ctl, HG_SV_CTL_BYTES);  // (polled by scalar loads: hg_mega.hip sv_sload)
     if (!rc && spill_bytes) rc = ensure(c, S.spill, spill_bytes);
