@@ -116,7 +116,7 @@ public class HalogenRenderPass : ScriptableRenderPass
     readonly List<HalogenTriangle> triangles = new List<HalogenTriangle>();
     readonly List<BVHEntry> blas = new List<BVHEntry>();
     readonly List<HalogenMaterial> seenMaterials = new List<HalogenMaterial>();
-    // the geometry generation of hg_upload_scene_gen: bumped whenever the mesh registry's members (instance, triangle
+    // the geometry generation of hg_upload_scene_gen: bumped whenever the mesh registry's members (manager ID, triangle
     // count, BVH size, in order) differ from the last upload's; equal, it vouches for the 78 MB of triangles and BVH
     // entries the reference re-uploads on every camera move (RP:262-268, 296-299), which the library then skips comparing
     readonly List<long> geometrySignature = new List<long>();
@@ -351,7 +351,7 @@ public class HalogenRenderPass : ScriptableRenderPass
             triangles.AddRange(m.GetPackedTriangles());
             meshes.Add(m.GetRefreshedMeshData(mat, triOffset, nodeOffset));
             blas.AddRange(m.GetBVH());
-            signature.Add(m.GetInstanceID());
+            signature.Add(m.GetID());  // new on every OnEnable, when the mesh re-reads its triangles (RayTracingManager.cs:74-79)
             signature.Add(triangles.Count - triOffset);
             signature.Add(blas.Count - nodeOffset);
         }

@@ -48,7 +48,7 @@
 #include "hg_tiling.h"
 
 namespace {
-constexpr int kAgreeInts = 5;  // W, H, -W, -H, bad tiling (max-reduced: equal on every rank iff max == -max(-v))
+constexpr int kAgreeInts = 6;  // W, H, -W, -H, bad tiling, lost frame (max-reduced: equal on every rank iff max == -max(-v))
 }
 
 struct hg_comm {
@@ -250,8 +250,9 @@ int check_member(hg_comm* m, const hg_comm::Member& mb, int32_t W, int32_t H) {
     return HG_OK;
 }
 
-// RCCL transport: every rank of the communicator contributes (W, H, -W, -H, bad) and max-reduces; all ranks then hold
-// the same verdict, so a mismatch fails the gather everywhere before any send / receive is posted.
+// RCCL transport: every rank of the communicator contributes (W, H, -W, -H, bad, lost) and max-reduces; all ranks then
+// hold the same verdict, so a mismatch, or an accumulation invalidated by a lost render-server frame on any rank
+// (HG_E_FRAME_LOST), fails the gather everywhere before any send / receive is posted.
 int agree_on_target(hg_comm* m, int32_t& W, int32_t& H) {
     for (auto& mb : m->members) {
         const hg_ctx* c = mb.ctx;
@@ -261,6 +262,7 @@ int agree_on_target(hg_comm* m, int32_t& W, int32_t& H) {
         v[2] = -c->W;
         v[3] = -c->H;
         v[4] = member_mismatch(m, mb);
+        v[5] = hg_ctx_lost(mb.ctx) ? 1 : 0;
         HG_CHIP(m, hipSetDevice(c->device));
         HG_CHIP(m, hipEventRecord(mb.ready, c->stream));
         HG_CHIP(m, hipMemcpyAsync(mb.agree_dev, v, kAgreeInts * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
@@ -298,6 +300,8 @@ int agree_on_target(hg_comm* m, int32_t& W, int32_t& H) {
                              mb.ctx->rank, mb.ctx->n_ranks, mb.ctx->W, mb.ctx->H, mb.rank, m->n_ranks);
         return cfail(m, HG_E_COMM, "a peer rank's context is not tiled for this communicator or has no target");
     }
+    if (r[5] != 0)
+        return cfail(m, HG_E_FRAME_LOST, "a rank's accumulation is invalid: a render server frame was lost there");
     if (r[0] != -r[2] || r[1] != -r[3])
         return cfail(m, HG_E_COMM, "ranks disagree on the target size (widths %d..%d, heights %d..%d)", -r[2], r[0],
                      -r[3], r[1]);
@@ -496,6 +500,10 @@ int hg_comm_gather(hg_comm* m, int32_t root) {
     } else {
         for (const auto& mb : m->members)
             if (int rc = check_member(m, mb, W, H)) return rc;
+        for (const auto& mb : m->members)
+            if (hg_ctx_lost(mb.ctx))
+                return cfail(m, HG_E_FRAME_LOST, "rank %d: its accumulation is invalid (a render server frame was lost)",
+                             mb.rank);
     }
     const hg_ctx* c0 = m->members.front().ctx;
     const int32_t n = m->n_ranks;
@@ -599,6 +607,10 @@ int hg_comm_readback(hg_comm* m, float* rgba, size_t n_floats) {
     HG_CHIP(m, hipMemcpyAsync(rgba, m->image.p, size_t(m->W) * size_t(m->H) * sizeof(float4), hipMemcpyDeviceToHost,
                               rc->stream));
     HG_CHIP(m, hipStreamSynchronize(rc->stream));
+    for (const auto& mb : m->members)  // (a frame lost after the gather's agreement: the image is handed out, flagged)
+        if (hg_ctx_lost(mb.ctx))
+            return cfail(m, HG_E_FRAME_LOST, "rank %d: its accumulation is invalid (a render server frame was lost)",
+                         mb.rank);
     return HG_OK;
 }
 
@@ -625,6 +637,10 @@ int hg_comm_readback_end(hg_comm* m, const void** data, size_t* n_bytes, int32_t
     if (int rc = wait_streams(m, "hg_comm_readback_end", ev)) return rc;
     if (int e = hg_readback_end_data(m->root_ctx, data, n_bytes, format))
         return cfail(m, e, "%s", m->root_ctx->err.c_str());
+    for (const auto& mb : m->members)
+        if (hg_ctx_lost(mb.ctx))
+            return cfail(m, HG_E_FRAME_LOST, "rank %d: its accumulation is invalid (a render server frame was lost)",
+                         mb.rank);
     return HG_OK;
 }
 

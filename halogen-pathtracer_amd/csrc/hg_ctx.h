@@ -88,7 +88,7 @@ struct hg_ctx {
         DevBuf ring;        // colour ring: ring_n frames of n_local_tiles * 64 float4
         DevBuf spill, tile_cost, tile_order, order_scratch;
         bool tile_cost_valid = false;
-        unsigned long long* host = nullptr;  // pinned: [0] the post word (frames | stop << 32), [1] a gate's timeout
+        unsigned long long* host = nullptr;  // pinned, coherent: the host words HG_SV_HOST_* (hg_layout.h)
         uint32_t ring_n = 0, posted = 0, cap = 0;
         uint32_t uses[HG_SV_RING] = {};     // frames posted to each ring slot in this lifetime
         hipEvent_t blended[HG_SV_RING] = {};  // after the blend of each ring slot's last frame
@@ -96,13 +96,24 @@ struct hg_ctx {
         hg_params params{};   // the parameters it was started with (frameCount: its first frame)
         int32_t kernel_variant = 0, descent_t = 0;
         HgKernelParams kp{};  // the launch's parameters (the blends read acc / ring / first_frame)
-        double last_post_s = 0.0;  // host clock of the last post
+        int32_t idle_us = HG_SV_IDLE_US;  // HG_OPT_SERVER_IDLE_US
+        int64_t gate_us = -1;             // HG_OPT_SERVER_GATE_US (< 0: the default, 30 s)
 #if HG_SV_DIAG_TIMES
         double post_s[256] = {};  // (analysis builds) host clock of each post
 #endif
     } sv;
     int32_t server_on = 1;  // HG_OPT_SERVER
     uint64_t server_launches = 0, server_frames = 0;
+    uint64_t server_refused = 0;  // posts that met a closing server (the close handshake), re-posted to a new one
+    // Lost frames (a server frame's gate gave up, hg_server_gate): the gate raises `lost` (uncached device memory), and
+    // every later blend into the accumulator is skipped; the host marks the accumulator invalid (acc_lost) when it reads
+    // the gate's host word and the frame belongs to the current accumulation (acc_epoch: advanced by every clear,
+    // checkpoint load and reallocation, which also reset both).  While acc_lost, hg_render and every readback / copy /
+    // gather of the accumulator return HG_E_FRAME_LOST.
+    DevBuf lost;
+    uint32_t acc_epoch = 0;
+    bool acc_lost = false;
+    uint64_t frames_lost = 0;
     // The server serves only a host that runs ahead: each render call records call_done[calls & 1] on `stream` after
     // its frames' blends, so at a call the event of the call before last tells whether the GPU still works on it
     hipEvent_t call_done[2] = {};
@@ -147,6 +158,8 @@ struct hg_ctx {
 
 // Launch the held frames of a context, if any (hg_runtime.hip; every entry point but hg_render calls it first)
 int hg_ctx_flush(hg_ctx* c);
+// The context's accumulation is invalid (a render server frame was lost; reads the gates' report first)
+bool hg_ctx_lost(hg_ctx* c);
 // Enqueue a display readback (hg_readback_begin_format) from the accumulator (rows == nullptr) or from a row-major
 // float4 image of the target's size on the context's device; and the copy event of the oldest outstanding one
 int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format);

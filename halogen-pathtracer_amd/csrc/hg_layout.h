@@ -142,15 +142,18 @@
 // 128-B line of its own: the 8 unit heads (as above), then HG_SV_MIRRORS copies of the device mirror of the host's post
 // word (u64, raised by atomic max by whichever wave read the host word; an idle
 // wave reads copy blockIdx.x % HG_SV_MIRRORS: the polling of thousands of idle waves spread over as many lines), one
-// host-poll ticket per XCD (blockIdx.x % 8), and the count of waves that left (diagnostics)
+// host-poll ticket per XCD (blockIdx.x % 8), the count of waves that left (read by the gates: a frame whose count is
+// short once every wave has left is lost), and the closing word (0 open, 1 closing: the one wave that won it runs the
+// close handshake, hg_mega.hip sv_close)
 #define HG_SV_MIRRORS 16u
 #define HG_SV_MIRROR_WORD 288u
 #define HG_SV_TICKET_WORD (HG_SV_MIRROR_WORD + 32u * HG_SV_MIRRORS)
 #define HG_SV_EXIT_WORD (HG_SV_TICKET_WORD + 32u * 8u)  // waves of the server that left | grid << 32
+#define HG_SV_CLOSE_WORD (HG_SV_EXIT_WORD + 32u)
 #ifndef HG_SV_DIAG_TIMES
 #define HG_SV_DIAG_TIMES 0  // analysis builds: per frame (< 256) the device time of its first claim and its last count
 #endif
-#define HG_SV_DIAG_WORD (HG_SV_EXIT_WORD + 32u)
+#define HG_SV_DIAG_WORD (HG_SV_CLOSE_WORD + 32u)
 #define HG_SV_CTL_BYTES ((HG_SV_DIAG_WORD + (HG_SV_DIAG_TIMES ? 1024u : 0u)) * 4u)
 #ifndef HG_SV_POLL_TICKS
 #define HG_SV_POLL_TICKS 200u  // 2 us between reads of the host word over PCIe, per XCD
@@ -171,6 +174,17 @@
 #define HG_SV_RING 16  // colour ring slots of the render server (frames traced ahead of their blend), at most
 #endif
 #define HG_SV_STOP (1ull << 32)  // the post word's stop flag (posted frames in the low 32 bits)
+// The host words of a server (pinned, coherent; u64 each): the post word (frames posted | HG_SV_STOP), the lost-frame
+// word (a gate that gave up: HG_SV_LOST | the accumulator epoch of its frame), the closing word (raised by the wave
+// that closes the server, before it reads the post word) and the close word (the post word as that wave read it, with
+// HG_SV_STOP, | HG_SV_CLOSED once written)
+#define HG_SV_HOST_POST 0
+#define HG_SV_HOST_LOST 1
+#define HG_SV_HOST_CLOSING 2
+#define HG_SV_HOST_CLOSED 3
+#define HG_SV_CLOSED (1ull << 33)
+#define HG_SV_LOST (1ull << 32)
+#define HG_SV_IDLE_US 200000  // default HG_OPT_SERVER_IDLE_US: the server closes after this long with nothing posted
 #ifndef HG_REGEN_ITEMS
 #define HG_REGEN_ITEMS 1  // regenerating kernel: (pixel, frame) item scheduling (0: the A/B build of make noitems)
 #endif
@@ -240,11 +254,11 @@ struct HgKernelParams {
     // streaming launches without the queue and without a frame split: each wave traces wave_units consecutive units
     // of the cost order (1: one tile per wave), its lanes taking their items one after another (UnitItems)
     uint32_t wave_units;
-    // render server: the host's post word in pinned host memory (frames posted | stop << 32), read by the device
+    // render server: the host words in pinned host memory (HG_SV_HOST_*; [0] the post word, frames posted | stop << 32)
     const unsigned long long* __restrict__ sv_post;
     uint32_t sv_ring;        // colour ring slots (a power of two)
     uint32_t sv_frames_cap;  // frames the server may trace in its lifetime (n_local_tiles * frames < 2^31)
-    uint32_t sv_idle_ticks;  // a wave idle this long (100-MHz s_memrealtime ticks) with nothing posted leaves
+    uint32_t sv_idle_ticks;  // nothing posted for this long (100-MHz s_memrealtime ticks): a wave closes the server
     uint32_t sv_div_magic, sv_div_shift;  // unit -> frame: u / n_local_tiles = umulhi(u, magic) >> shift (u < 2^31)
     // tiling
     int32_t tiles_x, rank, n_ranks, n_local_tiles;

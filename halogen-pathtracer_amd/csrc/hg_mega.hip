@@ -664,6 +664,15 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
     }
 }
 
+// A word of uncached device memory read by a scalar load that bypasses the scalar cache (p uniform: a kernel argument).
+// The blends read the context's lost word so (hg_server_gate: once a server frame was lost, every later blend into the
+// accumulator is skipped until a clear or a checkpoint load resets the word), one load per workgroup.
+__device__ __forceinline__ uint32_t sload_u32(const uint32_t* p) {  // (p uniform: a kernel argument)
+    uint32_t v;
+    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
 // Frame-parallel epilogue: acc = acc*(1-w) + c_f*w for f in frame order (AccumulationShader.shader:33), exactly the
 // per-frame blend the kernels do themselves when they blend in place.
 // Over the [slot][frame] colour layout each wave owns 64 slots (a tile) and moves their colours 8 frames at
@@ -671,7 +680,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_MEGA_WAVES) void hg_trace_regen_ke
 // instead of 64 lanes on 64 lines; then each lane blends its slot's 8 frames in frame order.
 __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ acc, const float4* __restrict__ colors,
                                                           uint32_t n_slots, int32_t n_frames, int32_t first_frame,
-                                                          int32_t accumulate) {
+                                                          int32_t accumulate, const uint32_t* lost) {
+    if (sload_u32(lost)) return;
     constexpr uint32_t kRow = 9;  // float4 per slot row: 8 frames + 1 pad (spreads the lanes' rows over the banks)
     __shared__ float4 stage[4][64 * kRow];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -709,7 +719,8 @@ __global__ __launch_bounds__(256) void hg_blend_frames_sm(float4* __restrict__ a
 // the trace to wind down: 0.7 ms per 1-frame blend on C3).  Same operations in the same order.
 __global__ __launch_bounds__(64) void hg_blend_frames_lean(float4* __restrict__ acc, const float4* __restrict__ colors,
                                                            uint32_t n_slots, int32_t n_frames, int32_t first_frame,
-                                                           int32_t accumulate) {
+                                                           int32_t accumulate, const uint32_t* lost) {
+    if (sload_u32(lost)) return;
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n_slots) return;
     float4 a = acc[i];
@@ -726,16 +737,16 @@ __global__ __launch_bounds__(64) void hg_blend_frames_lean(float4* __restrict__ 
     acc[i] = a;
 }
 
-hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream) {
+hipError_t hg_launch_blend_frames(const HgKernelParams& kp, const uint32_t* lost, hipStream_t stream) {
     const uint32_t n_slots = uint32_t(kp.n_local_tiles) * 64u;
     if (n_slots == 0) return hipSuccess;
     if (kp.n_frames <= HG_QUEUE_MAX_FRAMES) {
         hipLaunchKernelGGL(hg_blend_frames_lean, dim3((n_slots + 63) / 64), dim3(64), 0, stream, kp.acc, kp.frame_color,
-                           n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+                           n_slots, kp.n_frames, kp.first_frame, kp.accumulate, lost);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(hg_blend_frames_sm, dim3((n_slots + 255) / 256), dim3(256), 0, stream, kp.acc,
-                       kp.frame_color, n_slots, kp.n_frames, kp.first_frame, kp.accumulate);
+                       kp.frame_color, n_slots, kp.n_frames, kp.first_frame, kp.accumulate, lost);
     return hipGetLastError();
 }
 
@@ -919,9 +930,14 @@ __device__ __forceinline__ void slot_pixel(const HgKernelParams& kp, uint32_t sl
 //             memory (no XCD's L2 holds their lines): the gate kernel on the context stream waits for the count, and
 //             the blend after it reads the colours, whichever XCD wrote them (plain stores then the drain, then the
 //             count's atomic: the colours are in memory before the count says so).
-//   leaving   a wave with no item and no posted unit left waits (s_sleep); it leaves once the stop flag is set and
-//             nothing posted is left to claim, or after sv_idle_ticks with nothing posted (the host restarts a server
-//             that has been idle for less than half of that instead of posting to it).
+//   leaving   a wave with no item and no posted unit left waits (s_sleep); it leaves once the stop flag is in its view
+//             and nothing posted is left to claim.  The stop flag comes from the host (server_stop), or from the close
+//             handshake: after sv_idle_ticks with nothing new posted, one wave closes the server (sv_close).  It raises
+//             the closing word in host memory, then reads the post word, and publishes what it read with the stop flag
+//             (to the host and to every mirror): every frame it read is traced before the waves leave.  The host raises
+//             the post word, then reads the closing word; a post that finds it raised counts only if the closing wave
+//             read it (both sides store, then load: at least one sees the other's store), else the host restarts the
+//             server and posts there.  So no posted frame can meet a server whose waves have all left.
 // Only the lane 0 of a wave runs these (the whole wave converged at the loop top).
 // Per-wave LDS state (lane 0 reads and writes it; the constants are copied from the kernel arguments once, so that no
 // server value stays in a scalar register across the kernel's loop: its scalar registers are all taken, and every
@@ -1140,12 +1156,33 @@ __device__ bool sv_refill(const HgKernelParams& kp) {
     }
     return cnt >= lds_get(hg_qu[a ^ 1u].end) && cnt >= lds_get(hg_qu[a].end);
 }
+// The close handshake (lane 0 of an idle wave, after sv_idle_ticks with nothing new posted).  One wave wins the closing
+// word of the control block; it raises the host's closing word, then reads the post word (system scope, sequentially
+// consistent: the store is visible to the host before the load is performed), and publishes the post word it read with
+// the stop flag, to the host (the close word, HG_SV_CLOSED) and to every mirror (atomic max: the stop flag outranks
+// every post word without it, so a poller that read a later post word cannot raise a view past it).  Every wave then
+// drains the frames of that view and leaves.  The host's side is hg_runtime.hip server_post.
+__device__ void sv_close(const HgKernelParams& kp) {
+    uint32_t* const word = kp.queue + HG_SV_CLOSE_WORD;
+    if (ld_agent(word) != 0u || atomicCAS(word, 0u, 1u) != 0u) return;  // another wave closes it
+    unsigned long long* const host = sv_ptr<unsigned long long>(lds_get(hg_sv.post_lo), lds_get(hg_sv.post_hi));
+    __hip_atomic_store(host + HG_SV_HOST_CLOSING, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    const unsigned long long p = __hip_atomic_load(host + HG_SV_HOST_POST, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long fin = (p & 0xFFFFFFFFull) | HG_SV_STOP;
+    __hip_atomic_store(host + HG_SV_HOST_CLOSED, fin | HG_SV_CLOSED, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t m = 0; m < HG_SV_MIRRORS; ++m)
+        __hip_atomic_fetch_max(sv_word64(kp, HG_SV_MIRROR_WORD + 32u * m), fin, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
 // A wave with no path: poll (the host word through the ticket) and wait until a unit is posted (returns 0: refill) or
-// it may leave (1)
+// it may leave (1): the stop flag in its view and nothing posted left to claim.  A wave that saw nothing new posted for
+// sv_idle_ticks closes the server (sv_close); it never leaves on its own clock.
 __device__ uint32_t sv_wait(const HgKernelParams& kp) {
     hg_wave_cost[threadIdx.x >> 6] = nullptr;  // the wait is no tile's cost
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t seen = HG_NONE;  // the view at which the heads were last read
+    uint32_t idle_view = lds_get(hg_sv.view);  // the view at t0 (a new post restarts the idle clock)
     for (uint32_t spin = 0;; ++spin) {
         // one coherent load per spin (this wave's mirror copy); the host word through the ticket every few spins
         const uint32_t view = (spin % HG_SV_POLL_EVERY) == 0u ? sv_poll(kp) : sv_view(kp);
@@ -1164,7 +1201,13 @@ __device__ uint32_t sv_wait(const HgKernelParams& kp) {
             return 0u;
         }
         if (lds_get(hg_sv.stop)) return 1u;  // the final post word: nothing posted is left to claim
-        if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(lds_get(hg_sv.idle_ticks))) return 1u;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (view != idle_view) {
+            idle_view = view;
+            t0 = now;
+        } else if (now - t0 > uint64_t(lds_get(hg_sv.idle_ticks))) {
+            sv_close(kp);  // (then the stop flag reaches this wave's view through the mirrors)
+        }
         // short sleeps between the first polls, then longer ones (s_sleep counts 64 clocks)
         if (spin < HG_SV_SPIN_SHORT) __builtin_amdgcn_s_sleep(HG_SV_SLEEP_SHORT);
         else __builtin_amdgcn_s_sleep(HG_SV_SLEEP_LONG);
@@ -1434,8 +1477,12 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
     }
     if constexpr (kQueue) record_tile_cost(lane);
     else items.record_cost(kp, lane);
-    if constexpr (kServer) {  // (diagnostics, hg_destroy under HALOGEN_SERVER_TRACE) waves out | grid << 32
+    if constexpr (kServer) {  // waves out | grid << 32 (the gates: a frame still short once all left is lost)
         if (lane == 0u) {
+            // after this wave's frame counts (its last sv_flush) have completed in memory
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
             __hip_atomic_store(kp.queue + HG_SV_EXIT_WORD + 1u, gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(kp.queue + HG_SV_EXIT_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1526,30 +1573,40 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp_in, int block, bool co
 }
 
 // The render server's per-frame work on the context stream (hg_runtime.hip server_post): the gate waits until the
-// frame's ring-slot count reaches `target` (one wave; agent-scope polls with a sleep, bounded: after `timeout_ticks`
-// it records the failure in the host-visible error word and returns), then the blend reads the frame's colours from
+// frame's ring-slot count reaches `target` (one wave; agent-scope polls with a sleep).  It gives up when every wave of
+// the server has left with the count still short (the frame can no longer complete), or after `timeout_ticks`: then
+// the frame is lost, and the gate raises the context's lost word (device memory: every later blend into the
+// accumulator is skipped, until a clear or a checkpoint load resets it) and the host's lost-frame word (HG_SV_LOST |
+// the accumulator epoch of the frame: the host marks the accumulator invalid).  The blend reads the frame's colours from
 // the uncached ring and blends them into the accumulator: acc*(1-w) + c*w, w = 1/FrameCount
 // (AccumulationShader.shader:33), the same operations as every other blend.  Both fit beside the server's waves
 // (64-thread groups, no LDS, few registers).
 __global__ __launch_bounds__(64) void hg_server_gate(const uint32_t* __restrict__ done, uint32_t target,
-                                                     uint64_t timeout_ticks, unsigned long long* __restrict__ err) {
-    // (the whole wave polls with scalar loads of the uncached count: nothing on the vector-memory pipe of the CU it
-    // shares with the server's waves; sv_sload)
+                                                     uint64_t timeout_ticks, const unsigned long long* exitw,
+                                                     uint32_t* lost, unsigned long long* __restrict__ err,
+                                                     uint32_t epoch) {
+    // (the whole wave polls with scalar loads of uncached words: nothing on the vector-memory pipe of the CU it shares
+    // with the server's waves; sv_sload)
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spin = 0;; ++spin) {
-        uint32_t n;
-        asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(n) : "s"(done) : "memory");
-        if (n >= target) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-            if (threadIdx.x == 0) __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
+        if (sload_u32(done) >= target) return;
+        bool gone = false;
+        if ((spin & 15u) == 15u) {  // every server wave has left: a count still short now stays short
+            const unsigned long long w = sv_sload(exitw);
+            gone = (w >> 32) != 0ull && uint32_t(w) == uint32_t(w >> 32) && sload_u32(done) < target;
         }
+        if (gone || __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) break;
         if (spin < 256u) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(8);
     }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(lost, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, HG_SV_LOST | epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 __global__ __launch_bounds__(64) void hg_server_blend(float4* __restrict__ acc, const float4* __restrict__ colors,
-                                                      uint32_t n_slots, int32_t frame_count) {
+                                                      uint32_t n_slots, int32_t frame_count, const uint32_t* lost) {
+    if (sload_u32(lost)) return;  // a frame before this one was lost: the accumulator stays as it was
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n_slots) return;
     const float4 c = fc_load(colors + i);  // (uncached memory: the server's stores, whichever XCD made them)
@@ -1561,11 +1618,13 @@ __global__ __launch_bounds__(64) void hg_server_blend(float4* __restrict__ acc, 
 }
 hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_slots, int32_t frame_count,
                                   const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
-                                  unsigned long long* err, hipStream_t stream) {
-    hipLaunchKernelGGL(hg_server_gate, dim3(1), dim3(64), 0, stream, done, target, timeout_ticks, err);
+                                  const unsigned long long* exitw, uint32_t* lost, unsigned long long* err,
+                                  uint32_t epoch, hipStream_t stream) {
+    hipLaunchKernelGGL(hg_server_gate, dim3(1), dim3(64), 0, stream, done, target, timeout_ticks, exitw, lost, err,
+                       epoch);
     if (n_slots)
         hipLaunchKernelGGL(hg_server_blend, dim3((n_slots + 63) / 64), dim3(64), 0, stream, acc, colors, n_slots,
-                           frame_count);
+                           frame_count, static_cast<const uint32_t*>(lost));
     return hipGetLastError();
 }
 

@@ -34,8 +34,9 @@ hipError_t hg_launch_mega_stream(const HgKernelParams& kp, int block, bool count
                                  bool server = false);
 hipError_t hg_launch_server_frame(float4* acc, const float4* colors, uint32_t n_slots, int32_t frame_count,
                                   const uint32_t* done, uint32_t target, uint64_t timeout_ticks,
-                                  unsigned long long* err, hipStream_t stream);
-hipError_t hg_launch_blend_frames(const HgKernelParams& kp, hipStream_t stream);
+                                  const unsigned long long* exitw, uint32_t* lost, unsigned long long* err,
+                                  uint32_t epoch, hipStream_t stream);
+hipError_t hg_launch_blend_frames(const HgKernelParams& kp, const uint32_t* lost, hipStream_t stream);
 hipError_t hg_launch_order_tiles(unsigned long long* cost, uint32_t* order, uint32_t n, void* scratch,
                                  unsigned long long* faults, hipStream_t stream);
 size_t hg_order_scratch_bytes(uint32_t n);
@@ -300,14 +301,14 @@ double host_seconds() {
 }
 
 // ---- the render server (hg_ctx::Server; device side hg_mega.hip kServer) ------------------------------------------
-// A server idle this long (no frame posted) is restarted instead of posted to: its waves leave after
-// kServerIdleTicks without work, and a post must never meet a server whose waves are leaving (a wave's idle time is at
-// most the host's time since its last post, checked just before each post, and a tenth of theirs).
-constexpr double kServerIdleS = 0.020;
-constexpr uint32_t kServerIdleTicks = 20000000u;           // 200 ms of the 100-MHz s_memrealtime
-constexpr uint64_t kGateTimeoutTicks = 30ull * 100000000ull;  // a frame's gate gives up after 30 s (reported)
-// (HALOGEN_SERVER_GATE_TIMEOUT_MS overrides it, for diagnostics: a shorter bound turns a lost frame into an error fast)
-uint64_t gate_timeout_ticks() {
+// The server closes itself after HG_OPT_SERVER_IDLE_US with nothing posted (the close handshake, hg_mega.hip sv_close:
+// no host clock is involved in whether a post is taken).  A frame's gate gives up after 30 s, or at once when every
+// wave of the server has left with the frame's count short: the frame is lost (reported, the accumulator invalid).
+constexpr uint64_t kGateTimeoutTicks = 30ull * 100000000ull;  // 100-MHz s_memrealtime
+// HG_OPT_SERVER_GATE_US, else HALOGEN_SERVER_GATE_TIMEOUT_MS (diagnostics: a shorter bound turns a stuck frame into an
+// error fast), else 30 s
+uint64_t gate_timeout_ticks(const hg_ctx* c) {
+    if (c->sv.gate_us >= 0) return uint64_t(c->sv.gate_us) * 100ull;
     static const uint64_t t = [] {
         const char* e = std::getenv("HALOGEN_SERVER_GATE_TIMEOUT_MS");
         const long long ms = e ? std::atoll(e) : 0;
@@ -328,12 +329,31 @@ void sv_trace(const char* fmt, ...) {
     va_end(ap);
 }
 
-// A gate's timeout (the frame's count never reached its target) reported once, as an error of the entry point
-int server_check(hg_ctx* c) {
-    if (c->sv.host && __atomic_load_n(&c->sv.host[1], __ATOMIC_SEQ_CST)) {
-        __atomic_store_n(&c->sv.host[1], 0ull, __ATOMIC_SEQ_CST);
-        return fail(c, HG_E_HIP, "render server: a frame's gate timed out (its trace never completed)");
-    }
+// A lost server frame, as its gate reported it in the host's lost-frame word (HG_SV_LOST | the accumulator epoch of the
+// frame): the accumulator is invalid if the frame belongs to the current accumulation (a clear, a checkpoint load or a
+// reallocation since has discarded it otherwise)
+void server_note_lost(hg_ctx* c) {
+    if (!c->sv.host) return;
+    const unsigned long long w = __atomic_exchange_n(&c->sv.host[HG_SV_HOST_LOST], 0ull, __ATOMIC_SEQ_CST);
+    if (!(w & HG_SV_LOST)) return;
+    c->frames_lost++;
+    sv_trace("a frame of accumulator epoch %u was lost (current epoch %u)", uint32_t(w), c->acc_epoch);
+    if (uint32_t(w) == c->acc_epoch) c->acc_lost = true;
+}
+// The error of every entry point that renders into or reads the accumulator while it is invalid
+int lost_check(hg_ctx* c) {
+    server_note_lost(c);
+    if (!c->acc_lost) return HG_OK;
+    return fail(c, HG_E_FRAME_LOST, "a render server frame was lost (its gate gave up before the frame completed): the "
+                                    "accumulation is invalid until hg_clear_accumulation or hg_set_accumulation");
+}
+// A new accumulation (clear, checkpoint load, reallocation), on the context stream after everything before it: lost
+// frames before it no longer matter, and the blends after it run again
+int reset_lost(hg_ctx* c) {
+    server_note_lost(c);
+    c->acc_epoch++;
+    c->acc_lost = false;
+    HG_HIP(c, hipMemsetAsync(c->lost.p, 0, sizeof(uint32_t), c->stream));
     return HG_OK;
 }
 
@@ -369,7 +389,7 @@ int server_stop(hg_ctx* c) {
     }
 #endif
     if (q != hipSuccess) return fail(c, HG_E_HIP, "render server: %s", hipGetErrorString(q));
-    return server_check(c);
+    return HG_OK;
 }
 
 // Wait for every stream of the context: the context stream and both trace streams (before device buffers that a
@@ -401,6 +421,8 @@ int alloc_target(hg_ctx* c) {
         L.tile_order_valid = false;
         L.frames_since_order = 0;
     }
+    c->sv.tile_cost_valid = false;  // (its buffer may be reallocated, or hold the old tiling's costs)
+    if (int rc = reset_lost(c)) return rc;
     const size_t bytes = size_t(c->n_local_tiles) * 64 * sizeof(float4);
     c->rb_pending = 0;  // quiesced: begun readbacks are complete, and their images die with the old size or tiling
     c->rb_next = 0;
@@ -458,7 +480,8 @@ int hg_create(int device, hg_ctx** out) {
         return HG_E_HIP;
     }
     c->n_cu = prop.multiProcessorCount;
-    if (hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes) != hipSuccess) {
+    if (ensure_uncached(c, c->lost, 128) != HG_OK || hipMemset(c->lost.p, 0, 128) != hipSuccess ||
+        hipMemset(c->counters_dev.p, 0, c->counters_dev.bytes) != hipSuccess) {
         hg_destroy(c);
         return HG_E_HIP;
     }
@@ -494,7 +517,7 @@ void hg_destroy(hg_ctx* c) {
     for (hg_ctx::TraceLane& L : c->lanes)
         if (L.stream) (void)hipStreamSynchronize(L.stream);
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tris, &c->normals, &c->cube,
-                      &c->acc, &c->counters_dev, &c->spill})
+                      &c->acc, &c->counters_dev, &c->spill, &c->lost})
         release(*b);
     for (hg_ctx::TraceLane& L : c->lanes) {
         for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.order_scratch, &L.queue})
@@ -860,7 +883,7 @@ int hg_clear_accumulation(hg_ctx* c) {
     if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
     if (c->acc.p) HG_HIP(c, hipMemsetAsync(c->acc.p, 0, c->acc.bytes, c->stream));
-    return HG_OK;
+    return reset_lost(c);
 }
 
 }  // extern "C"
@@ -883,21 +906,8 @@ int render_check(hg_ctx* c, int32_t n_frames) {
     return HG_OK;
 }
 
-// The server had work a moment ago: the blend of its last posted frame has not run yet, so that frame's gate has not
-// passed (or has just passed) and the waves tracing its last units live on for the kernel's idle time after them.
-// (Assumes the context stream never holds the gate back for anything near that long: the work queued there ahead of
-// it is other gates, blends, clears and readbacks.)
-bool server_recently_busy(const hg_ctx::Server& S) {
-    if (S.posted == 0u) return false;
-    const uint32_t s = (S.posted - 1u) & (S.ring_n - 1u);
-    if (!S.blend_valid[s]) return false;
-    const hipError_t q = hipEventQuery(S.blended[s]);
-    (void)hipGetLastError();  // hipErrorNotReady is a status here
-    return q == hipErrorNotReady;
-}
-
 // The server can take the frame of FrameCount `fc` next: running, started with these parameters and options, `fc`
-// continuing its chain, room left in its lifetime's unit numbering, not idle for long and its kernel still resident
+// continuing its chain, room left in its lifetime's unit numbering, not closing (sv_close) and its kernel still resident
 bool server_continues(hg_ctx* c, int32_t fc) {
     const hg_ctx::Server& S = c->sv;
     if (!S.running) return false;
@@ -905,7 +915,7 @@ bool server_continues(hg_ctx* c, int32_t fc) {
     p.frameCount = S.params.frameCount;
     if (std::memcmp(&p, &S.params, sizeof p) != 0 || int64_t(fc) != int64_t(S.params.frameCount) + int64_t(S.posted) ||
         S.kernel_variant != c->kernel || S.descent_t != c->descent_t || S.posted >= S.cap ||
-        (host_seconds() - S.last_post_s >= kServerIdleS && !server_recently_busy(S)))
+        __atomic_load_n(&S.host[HG_SV_HOST_CLOSING], __ATOMIC_SEQ_CST) != 0ull)
         return false;
     const hipError_t q = hipStreamQuery(S.stream);
     (void)hipGetLastError();
@@ -930,15 +940,14 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
         // itself (measured the same as the default pinned memory, tools/sweeps/sweep_r05_server.txt; this is the
         // memory type whose coherence the loads rely on)
         HG_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&S.host), 256, hipHostMallocMapped | hipHostMallocCoherent));
-        S.host[0] = S.host[1] = 0ull;
+        for (int k = 0; k < 4; ++k) S.host[k] = 0ull;
     }
     const uint32_t tiles = uint32_t(c->n_local_tiles);
     const size_t per_frame = size_t(tiles) * 64u * sizeof(float4);
     uint32_t ring = HG_SV_RING;
     while (ring > 2u && size_t(ring) * per_frame > (size_t(2) << 30)) ring >>= 1;
-    // waves per SIMD: fewer than the kernel's HG_STREAM_WAVES, so that the kernels the context stream runs between the
-    // server's frames (gates, blends, the display untile / pack) find registers and wave slots beside its persistent
-    // waves (HALOGEN_SERVER_WAVES overrides, 1..HG_STREAM_WAVES, for A/B)
+    // waves per SIMD: HG_SV_WAVES (HALOGEN_SERVER_WAVES overrides, 1..HG_STREAM_WAVES, for A/B; fewer leave wave slots
+    // to the kernels the context stream runs between the server's frames, and measured slower)
     static const uint32_t sv_waves = [] {
         const char* e = std::getenv("HALOGEN_SERVER_WAVES");
         const int v = e ? std::atoi(e) : 0;
@@ -1006,7 +1015,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     kp.sv_post = static_cast<const unsigned long long*>(post);
     kp.sv_ring = ring;
     kp.sv_frames_cap = std::min<uint32_t>(1u << 24, uint32_t((uint64_t(1) << 31) / std::max<uint32_t>(tiles, 1u)));
-    kp.sv_idle_ticks = kServerIdleTicks;
+    kp.sv_idle_ticks = uint32_t(std::min<uint64_t>(uint64_t(S.idle_us) * 100ull, 0xFFFFFFFFull));
     if ((tiles & (tiles - 1u)) == 0u) {  // unit -> frame (hg_mega.hip sv_frame): a shift, or a multiply-high and a shift
         kp.sv_div_magic = 0u;
         kp.sv_div_shift = uint32_t(__builtin_ctz(tiles));
@@ -1015,8 +1024,10 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
         kp.sv_div_magic = uint32_t(((uint64_t(1) << (32 + l)) + tiles - 1u) / tiles);
         kp.sv_div_shift = l;
     }
-    __atomic_store_n(&S.host[0], 0ull, __ATOMIC_SEQ_CST);
-    __atomic_store_n(&S.host[1], 0ull, __ATOMIC_SEQ_CST);
+    // (the lost-frame word is not reset: a gate of the last lifetime may still report into it)
+    __atomic_store_n(&S.host[HG_SV_HOST_POST], 0ull, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&S.host[HG_SV_HOST_CLOSING], 0ull, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&S.host[HG_SV_HOST_CLOSED], 0ull, __ATOMIC_SEQ_CST);
     HG_HIP(c, hg_launch_mega_stream(kp, 64, c->counters_on != 0, S.stream, true));
     S.running = true;
     S.ring_n = ring;
@@ -1031,16 +1042,17 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     S.kernel_variant = c->kernel;
     S.descent_t = c->descent_t;
     S.kp = kp;
-    S.last_post_s = host_seconds();
     c->server_launches++;
     sv_trace("start: FrameCount %d, %u tiles, ring %u, grid %u", fc, tiles, ring, grid);
     return HG_OK;
 }
 
-// Post the next frame to the server: its gate + blend on the context stream (in frame order, like every other blend),
-// then the post word.  Frames run at most ring_n ahead of their blends (the host waits for the blend of the frame
-// ring_n back before reusing its ring slot); HG_E_UNSUPPORTED (nothing posted) when that wait left the server idle too
-// long to post to.
+// Post the next frame to the server, then its gate + blend on the context stream (in frame order, like every other
+// blend).  Frames run at most ring_n ahead of their blends (the host waits for the blend of the frame ring_n back before
+// reusing its ring slot).  The post is the host's half of the close handshake (hg_mega.hip sv_close): raise the post
+// word, then read the closing word.  Not raised: the post is taken (a wave that closes later reads the post word after
+// this store).  Raised: the post is taken only if the closing wave's read of the post word included it (the close
+// word); else HG_E_UNSUPPORTED, nothing queued: the caller restarts the server and posts there.
 int server_post(hg_ctx* c) {
     hg_ctx::Server& S = c->sv;
     const uint32_t k = S.posted, s = k & (S.ring_n - 1u);
@@ -1048,34 +1060,51 @@ int server_post(hg_ctx* c) {
         sv_trace("post %u: waiting for the blend of frame %u", k, k - S.ring_n);
         HG_HIP(c, hipEventSynchronize(S.blended[s]));
         sv_trace("post %u: waited", k);
-        if (host_seconds() - S.last_post_s >= kServerIdleS && !server_recently_busy(S)) return HG_E_UNSUPPORTED;
+    }
+    __atomic_store_n(&S.host[HG_SV_HOST_POST], static_cast<unsigned long long>(k + 1u), __ATOMIC_SEQ_CST);
+    if (__atomic_load_n(&S.host[HG_SV_HOST_CLOSING], __ATOMIC_SEQ_CST) != 0ull) {
+        // the closing wave publishes the post word it read right after reading it (bounded wait: a wave that raised
+        // the closing word is running its next few instructions)
+        unsigned long long fin;
+        const double t0 = host_seconds();
+        while (!((fin = __atomic_load_n(&S.host[HG_SV_HOST_CLOSED], __ATOMIC_SEQ_CST)) & HG_SV_CLOSED)) {
+            if (host_seconds() - t0 > 10.0) return fail(c, HG_E_HIP, "render server: the closing wave never published");
+            std::this_thread::yield();
+        }
+        if (uint32_t(fin) < k + 1u) {
+            c->server_refused++;
+            sv_trace("post %u: refused (the server closed at %u frames)", k, uint32_t(fin));
+            return HG_E_UNSUPPORTED;
+        }
+        sv_trace("post %u: taken by a closing server", k);
     }
     S.uses[s]++;
     const uint32_t tiles = uint32_t(c->n_local_tiles), n_slots = tiles * 64u;
     void* err = nullptr;
-    HG_HIP(c, hipHostGetDevicePointer(&err, S.host + 1, 0));
+    HG_HIP(c, hipHostGetDevicePointer(&err, S.host + HG_SV_HOST_LOST, 0));
     HG_HIP(c, hg_launch_server_frame(static_cast<float4*>(c->acc.p),
                                      static_cast<const float4*>(S.ring.p) + size_t(s) * n_slots, n_slots,
                                      S.kp.first_frame + int32_t(k), static_cast<const uint32_t*>(S.done.p) + 32u * s,
-                                     S.uses[s] * tiles, gate_timeout_ticks(), static_cast<unsigned long long*>(err),
-                                     c->stream));
+                                     S.uses[s] * tiles, gate_timeout_ticks(c),
+                                     reinterpret_cast<const unsigned long long*>(static_cast<const uint32_t*>(S.ctl.p) +
+                                                                                 HG_SV_EXIT_WORD),
+                                     static_cast<uint32_t*>(c->lost.p), static_cast<unsigned long long*>(err),
+                                     c->acc_epoch, c->stream));
     HG_HIP(c, hipEventRecord(S.blended[s], c->stream));
     S.blend_valid[s] = true;
     S.posted = k + 1u;
-    __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted), __ATOMIC_SEQ_CST);
 #if HG_SV_DIAG_TIMES
     if (k < 256u) S.post_s[k] = host_seconds();
 #endif
-    S.last_post_s = host_seconds();
     c->server_frames++;
     sv_trace("posted %u (slot %u, target %u)", k, s, S.uses[s] * tiles);
     return HG_OK;
 }
 
 // n_frames frames from FrameCount = params.frameCount through the server (started or restarted as needed).  A first
-// HG_E_UNSUPPORTED (no stream of its own) falls back to launches; nothing was posted then.
+// HG_E_UNSUPPORTED (no stream of its own) falls back to launches; nothing was posted then.  A post refused by a closing
+// server restarts it (bounded: a server closes only after HG_OPT_SERVER_IDLE_US with nothing posted).
 int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
-    if (int rc = server_check(c)) return rc;
     for (int32_t f = 0; f < n_frames; ++f) {
         const int32_t fc = c->params.frameCount + f;
         for (int attempt = 0;; ++attempt) {
@@ -1091,7 +1120,7 @@ int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
                 if (rc) return rc;
                 break;
             }
-            if (attempt) return fail(c, HG_E_HIP, "render server: a fresh server refused a post");
+            if (attempt >= 64) return fail(c, HG_E_HIP, "render server: 64 fresh servers in a row refused a post");
         }
     }
     return HG_OK;
@@ -1415,7 +1444,8 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 }
                 if (e == hipSuccess) e = hipEventRecord(L.traced, L.stream);
                 if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, L.traced, 0);
-                if (e == hipSuccess) e = hg_launch_blend_frames(kc, c->stream);  // in frame order, on the context stream
+                if (e == hipSuccess)  // in frame order, on the context stream
+                    e = hg_launch_blend_frames(kc, static_cast<const uint32_t*>(c->lost.p), c->stream);
                 if (e == hipSuccess) e = hipEventRecord(L.blended, c->stream);
                 L.blend_pending = e == hipSuccess;
                 done += kc.n_frames;
@@ -1455,6 +1485,11 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
 }
 
 }  // namespace
+
+bool hg_ctx_lost(hg_ctx* c) {
+    server_note_lost(c);
+    return c->acc_lost;
+}
 
 int hg_ctx_flush(hg_ctx* c) {
     if (!c || c->pending_frames == 0) return HG_OK;
@@ -1606,11 +1641,10 @@ int hg_readback_end_data(hg_ctx* c, const void** data, size_t* n_bytes, int32_t*
     const int k = (c->rb_next - c->rb_pending + c->rb_depth) % c->rb_depth;  // the oldest begun
     HG_HIP(c, hipEventSynchronize(c->image_copied[k]));
     c->rb_pending--;
-    if (int rc = server_check(c)) return rc;
     *data = c->image_host[k];
     if (n_bytes) *n_bytes = c->image_host_bytes[k];
     if (format) *format = c->image_host_format[k];
-    return HG_OK;
+    return lost_check(c);  // (the image is handed out either way: the accumulation through the last frame blended)
 }
 
 int hg_readback_end(hg_ctx* c, const float** rgba, size_t* n_floats) {
@@ -1646,6 +1680,7 @@ int hg_pack_display(const float* rgba, size_t n_pixels, int32_t format, void* ou
 int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (!c) return HG_E_INVALID;
     if (int rc = render_check(c, n_frames)) return rc;
+    if (int rc = lost_check(c)) return rc;
     if (n_frames == 0) return HG_OK;
     accumulate = accumulate ? 1 : 0;
     if (c->pending_frames > 0 && (accumulate != c->pending_acc || int64_t(c->pending_frames) + n_frames > INT32_MAX))
@@ -1663,7 +1698,8 @@ int hg_synchronize(hg_ctx* c) {
     if (int rc = hg_ctx_flush(c)) return rc;
     if (int rc = set_device(c)) return rc;
     if (int rc = quiesce(c)) return rc;
-    return drain_events(c);
+    if (int rc = drain_events(c)) return rc;
+    return lost_check(c);
 }
 
 int32_t hg_local_tile_count(const hg_ctx* c) { return c ? c->n_local_tiles : 0; }
@@ -1679,8 +1715,8 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
         if (int rc = untile_async(c, &bytes)) return rc;
         HG_HIP(c, hipMemcpyAsync(rgba, c->image.p, bytes, hipMemcpyDeviceToHost, c->stream));
         HG_HIP(c, hipStreamSynchronize(c->stream));
-        if (int rc = server_check(c)) return rc;
-        return drain_events(c);
+        if (int rc = drain_events(c)) return rc;
+        return lost_check(c);  // (the image is written either way: the accumulation through the last frame blended)
     }
     // this rank's pixels only (the others are left untouched): the tiles are repacked on the host
     std::vector<float4> tiles(size_t(c->n_local_tiles) * 64);
@@ -1702,7 +1738,7 @@ int hg_readback(hg_ctx* c, float* rgba, size_t n_floats) {
             d[3] = v.w;
         }
     }
-    return HG_OK;
+    return lost_check(c);
 }
 
 int hg_set_accumulation(hg_ctx* c, const float* rgba, size_t n_floats, int32_t frame_count) {
@@ -1726,6 +1762,7 @@ int hg_set_accumulation(hg_ctx* c, const float* rgba, size_t n_floats, int32_t f
     }
     if (!tiles.empty())
         HG_HIP(c, hipMemcpyAsync(c->acc.p, tiles.data(), tiles.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    if (int rc = reset_lost(c)) return rc;
     HG_HIP(c, hipStreamSynchronize(c->stream));  // the staging vector dies at return
     c->params.frameCount = frame_count;
     return drain_events(c);
@@ -1740,7 +1777,8 @@ int hg_copy_tiles_device(hg_ctx* c, void* dst, size_t n_bytes) {
     HG_HIP(c, hipStreamSynchronize(c->stream));  // every render kernel retired before the copy engine reads acc
     if (need) HG_HIP(c, hipMemcpyAsync(dst, c->acc.p, need, hipMemcpyDeviceToDevice, c->stream));
     HG_HIP(c, hipStreamSynchronize(c->stream));
-    return drain_events(c);
+    if (int rc = drain_events(c)) return rc;
+    return lost_check(c);
 }
 
 int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
@@ -1776,6 +1814,9 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->scene_uploads_vouched = c->scene_uploads_vouched;
     out->server_launches = c->server_launches;
     out->server_frames = c->server_frames;
+    server_note_lost(c);
+    out->server_refused = c->server_refused;
+    out->frames_lost = c->frames_lost;
     return HG_OK;
 }
 
@@ -1866,6 +1907,13 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_SERVER:
             if (value < 0 || value > 2) return fail(c, HG_E_INVALID, "HG_OPT_SERVER %d: expected 0, 1 or 2", value);
             c->server_on = value;
+            return HG_OK;
+        case HG_OPT_SERVER_IDLE_US:
+            if (value < 0 || value > 40000000) return fail(c, HG_E_INVALID, "server idle time must be 0..40000000 us");
+            c->sv.idle_us = value;
+            return HG_OK;
+        case HG_OPT_SERVER_GATE_US:
+            c->sv.gate_us = value;  // (< 0: the default)
             return HG_OK;
         case HG_OPT_WAVE_UNITS:
             if (value < 0 || value > HG_WAVE_UNITS_LIMIT)

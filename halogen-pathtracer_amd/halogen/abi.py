@@ -86,7 +86,7 @@ class HgCounters(C.Structure):
                 ("scene_uploads", C.c_uint64), ("scene_uploads_skipped", C.c_uint64),
                 ("scene_uploads_partial", C.c_uint64), ("scene_uploads_vouched", C.c_uint64),
                 ("server_launches", C.c_uint64),
-                ("server_frames", C.c_uint64)]
+                ("server_frames", C.c_uint64), ("server_refused", C.c_uint64), ("frames_lost", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)
@@ -105,6 +105,10 @@ HG_OPT_READBACK_STREAM = 11
 HG_OPT_WAVE_UNITS = 12
 HG_OPT_LANE_PICK = 14
 HG_OPT_SERVER = 15
+HG_OPT_SERVER_IDLE_US = 16
+HG_OPT_SERVER_GATE_US = 17
+HG_E_INVALID, HG_E_HIP, HG_E_NOMEM, HG_E_NOSCENE, HG_E_NOTARGET, HG_E_UNSUPPORTED, HG_E_COMM = -1, -2, -3, -4, -5, -6, -7
+HG_E_FRAME_LOST = -8
 HG_READBACK_MAX = 16
 # display formats of readback_begin(format=...) (include/halogen_abi.h, csrc/hg_pack.h): bytes per pixel and numpy view
 HG_DISPLAY_RGBA32F, HG_DISPLAY_RGBA16F, HG_DISPLAY_R11G11B10F = 0, 1, 2
@@ -204,7 +208,9 @@ def lib() -> C.CDLL:
 
 
 class HalogenError(RuntimeError):
-    pass
+    def __init__(self, msg: str, rc: int = 0):
+        super().__init__(msg)
+        self.rc = rc  # the HG_E_* code (0 when not from an entry point)
 
 
 def _ptr(a) -> C.c_void_p:
@@ -249,7 +255,7 @@ class Context:
     def _check(self, rc: int, what: str):
         if rc != HG_OK:
             msg = lib().hg_last_error(self._h)
-            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -394,7 +400,7 @@ class Comm:
     def _check(self, rc: int, what: str):
         if rc != HG_OK:
             msg = lib().hg_comm_last_error(self._h)
-            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+            raise HalogenError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)
 
     @property
     def transport(self) -> int:

@@ -153,7 +153,7 @@ class HalogenRenderPass:
         self._prior_resolution = None
         self._scene_counts = (0, 0)
         self._cubemap_uploaded = False
-        # hg_upload_scene_gen's geometry generation: bumped whenever the scene's meshes (identity, triangle and node
+        # hg_upload_scene_gen's geometry generation: bumped whenever the scene's meshes (cache token, triangle and node
         # counts, in order) differ from the last upload's, so a camera move's re-upload compares only the small arrays
         self._geometry = (None, 0)
         self.rank, self.n_ranks = 0, 1
@@ -193,7 +193,7 @@ class HalogenRenderPass:
         packed = scene.pack() if hasattr(scene, "pack") else scene
         generation = 0  # a bare PackedScene: every array compared
         if hasattr(scene, "meshes") and hasattr(scene, "pack"):
-            sig = tuple((id(m), m.triangle_count, len(m.bvh)) for m in scene.meshes)
+            sig = tuple((m.cache_token, m.triangle_count, len(m.bvh)) for m in scene.meshes)
             if sig != self._geometry[0]:
                 self._geometry = (sig, self._geometry[1] + 1)
             generation = self._geometry[1]

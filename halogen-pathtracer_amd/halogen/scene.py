@@ -14,6 +14,7 @@ on packed values (1/subsurface * absorption, bounds centre/extents) is done in f
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import os
 from dataclasses import dataclass, field
 
@@ -93,6 +94,9 @@ def set_blas_builder(name: str) -> str:
     return prev
 
 
+_CACHE_TOKENS = itertools.count(1)
+
+
 class RayTracingMesh:
     """RayTracingMesh.cs: submesh-0 triangles, vertices and normals of a mesh + its transform + material.
 
@@ -115,6 +119,9 @@ class RayTracingMesh:
         self._cache()
 
     def _cache(self):
+        # a new token whenever the geometry is (re)cached, as the reference's manager ID is new on every OnEnable
+        # (RayTracingManager.cs:74-79): the pass's geometry generation keys on it (id() of a collected mesh is reused)
+        self.cache_token = next(_CACHE_TOKENS)
         L = abi.lib()
         n_tris = len(self.triangles)
         mn, mx = mesh_bounds_min_max(self.vertices) if len(self.vertices) else (np.zeros(3, f32), np.zeros(3, f32))

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 5
+#define HG_ABI_VERSION 6
 
 /* ----------------------------------------------------------------------------------------------
  * Reference host structs (byte-identical to the C# [Sequential] structs)
@@ -181,6 +181,10 @@ typedef struct hg_counters {
                                        vouched for by an unchanged geometry generation (hg_upload_scene_gen), not compared */
     uint64_t server_launches;       /* render server lifetimes started (HG_OPT_SERVER), since hg_create */
     uint64_t server_frames;         /* frames posted to a render server, since hg_create */
+    uint64_t server_refused;        /* posts that met a closing render server (its close handshake had not read them),
+                                       re-posted to a new lifetime; since hg_create */
+    uint64_t frames_lost;           /* render server frames whose gate gave up (never 0 on a healthy device: each makes
+                                       the accumulation invalid, HG_E_FRAME_LOST), since hg_create */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -193,7 +197,11 @@ enum {
     HG_E_NOSCENE = -4,
     HG_E_NOTARGET = -5,  /* hg_resize not called */
     HG_E_UNSUPPORTED = -6,
-    HG_E_COMM = -7       /* RCCL error (text from ncclGetErrorString) or a mismatched communicator */
+    HG_E_COMM = -7,      /* RCCL error (text from ncclGetErrorString) or a mismatched communicator */
+    HG_E_FRAME_LOST = -8 /* a render server frame never completed (HG_OPT_SERVER): its blend and every later one were
+                            skipped, and the accumulation is invalid until hg_clear_accumulation / hg_set_accumulation
+                            (hg_render refuses; the readbacks still hand out the accumulation through the last frame
+                            blended, and return this code) */
 };
 
 /* Kernel variants selectable with hg_set_option(ctx, HG_OPT_KERNEL, v); all produce bit-identical images.
@@ -231,7 +239,7 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
        HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
-       HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15 };
+       HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17 };
 /* HG_OPT_SERVER (default 1): hg_render calls of at most 8 accumulating frames on the streaming kernel (the reference's
  *   one dispatch per frame, RP:327) post their frames to a render server — persistent trace waves that outlive the call
  *   and take each posted frame's (tile, frame) units as soon as lanes free up, so one frame's last paths overlap the
@@ -242,7 +250,13 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
  *   1 (automatic) uses the server only while the host runs ahead of the GPU (the call before last still in flight on
  *   the device: a host that queues frames); a host that waits for each frame (a display at once or one frame behind)
  *   launches per call, which measured faster there.  2 = always (while the calls qualify).  0 = every call launches
- *   (the round-4 per-launch pipeline).  Same images either way. */
+ *   (the round-4 per-launch pipeline).  Same images either way.
+ * HG_OPT_SERVER_IDLE_US (default 200000): a server with nothing new posted for this long closes itself (its waves
+ *   leave the GPU).  Whether a post is taken never depends on a clock: one wave closes the server by a handshake with
+ *   the host's post (both store, then load), and a post the closing wave did not see is re-posted to a new server
+ *   (hg_counters.server_refused).  0..40000000; small values are for tests.
+ * HG_OPT_SERVER_GATE_US (default -1: 30 s): a server frame whose gate waits this long is lost (HG_E_FRAME_LOST); a
+ *   frame still short once every wave of its server has left is lost at once.  For tests and diagnostics. */
 /* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
  *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
  *   device image and copied on the context stream.  Same images either way. */

@@ -63,7 +63,12 @@ def test_library_exports_every_declared_symbol(built):
     missing = [s for s in declared if s not in exported]
     assert not missing, missing
     L = abi.lib()  # loads, binds every signature
-    assert L.hg_abi_version() == 5
+    assert L.hg_abi_version() == 6
+
+
+def test_error_codes_match_header(built):
+    declared = {k: int(v) for k, v in re.findall(r"\b(HG_E_\w+) = (-\d+)", HEADER.read_text())}
+    assert declared and all(getattr(abi, k) == v for k, v in declared.items()), declared
 
 
 def test_no_gpu_is_a_loud_error(built):

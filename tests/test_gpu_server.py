@@ -6,7 +6,8 @@ the streaming kernel post their frames to persistent trace waves that outlive th
 context stream behind a gate on that frame's completion count.  Every image here is compared bit for bit with the
 batched launch (or the committed golden and its counters), with the server off (every call its own launch), and across
 every event that stops or restarts the server: a new camera, a checkpoint, a clear, counters, an idle gap, a launch of
-another kind, readbacks in flight."""
+another kind, readbacks in flight; posts racing the server's close handshake; and a lost frame (its gate gave up), which
+must leave the accumulator as it was and make every readback report HG_E_FRAME_LOST until a clear."""
 import json
 import time
 from pathlib import Path
@@ -21,10 +22,12 @@ from test_gpu_parity import assert_bitwise, gpu_render
 GOLD = Path(__file__).resolve().parent / "golden"
 
 
-def _ctx(packed, params, cube=None, server=2, coalesce=1, tiling=None):
+def _ctx(packed, params, cube=None, server=2, coalesce=1, tiling=None, idle_us=None):
     W, H = int(params.screenParameters.x), int(params.screenParameters.y)
     ctx = abi.Context(0)
     ctx.set_option(abi.HG_OPT_SERVER, server)
+    if idle_us is not None:
+        ctx.set_option(abi.HG_OPT_SERVER_IDLE_US, idle_us)
     ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
     ctx.upload_scene(packed)
     if cube is not None:
@@ -140,8 +143,8 @@ def test_gpu_server_restarts_keep_the_image(gpu):
     """Every event that ends a server lifetime, mid-run, against the same call sequence with the server off: a camera
     move (set_params with a new camera and FrameCount 1, then clear, as ClearAccumulation does, RP:262-268), a
     checkpoint (set_accumulation), a clear alone (the server keeps running: the clear is ordered between blends), a
-    counters read, a launch of another kind (a 16-frame call), an idle gap longer than the server's, idle gaps that
-    restart a server still running (its counts not zero), an upload."""
+    counters read, a launch of another kind (a 16-frame call), short idle gaps (the server stays), an idle gap longer
+    than the server's idle time (it closes itself; the next post restarts it), an upload."""
     packed, params, cube, _, _ = cases.setup("dragon10_64x36")
     moved = cases.setup("dragon10_64x36")[1]
     moved.camLocalToWorld.m[12] += 0.05
@@ -168,9 +171,11 @@ def test_gpu_server_restarts_keep_the_image(gpu):
             frames(2)
             time.sleep(0.08)
             frames(2)
-            for _ in range(3):  # idle gaps past the host's restart threshold, well inside the waves' idle time: a
-                time.sleep(0.03)  # restart over a live server whose ring-slot counts are not zero
+            for _ in range(3):  # short idle gaps: the server stays (its ring-slot counts not zero)
+                time.sleep(0.03)
                 frames(3)
+            time.sleep(0.3)  # past HG_OPT_SERVER_IDLE_US (200 ms): the server has closed itself
+            frames(2)
             ctx.upload_scene(packed)
             frames(2)
             cnt = ctx.counters()
@@ -229,9 +234,9 @@ def test_gpu_server_full_size_c3_with_display(gpu):
     assert_bitwise(img, want[64], "C3 1080p, 64 frames through the server")
     for k in checks:
         assert np.array_equal(shown[k - 1], abi.pack_display(want[k], abi.HG_DISPLAY_R11G11B10F)), f"displayed frame {k}"
-    # (a few restarts allowed: the first display readbacks allocate their pinned host images, gaps that may exceed the
-    # host's 20-ms restart threshold while no frame is in flight; every frame still went through the server)
-    assert cnt["server_launches"] <= 4 and cnt["server_frames"] == 64, cnt
+    # one lifetime: whether a post is taken depends on no host clock (the close handshake), and no gap here reaches the
+    # server's 200-ms idle time
+    assert cnt["server_launches"] == 1 and cnt["server_frames"] == 64, cnt
 
 
 @pytest.mark.gpu
@@ -258,3 +263,78 @@ def test_gpu_server_automatic_engages_only_ahead(gpu):
             assert cnt["server_launches"] == 0, cnt
         else:
             assert cnt["server_launches"] >= 1 and cnt["server_frames"] >= 16, cnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idle_us", [0, 30])
+def test_gpu_server_posts_racing_the_close_handshake(gpu, idle_us):
+    """HG_OPT_SERVER_IDLE_US 0 / 30: the server closes itself (sv_close) whenever it has nothing new for that long, so
+    nearly every one-frame post of this small image meets a server that is closing or gone.  A post the closing wave
+    did not read is refused and re-posted to a new lifetime (hg_counters.server_refused); one it did read is traced
+    before the waves leave.  200 frames, one per call and in fours, equal the batched launch bit for bit, and no frame
+    is lost (a lost one would make the readback fail with HG_E_FRAME_LOST)."""
+    packed, params, cube, _, _ = cases.setup("dragon10_64x36")
+    frames = 200
+    ref, rc = gpu_render(packed, params, frames, True, cube)
+    for per_call in (1, 4):
+        ctx, W, H = _ctx(packed, params, cube, idle_us=idle_us)
+        with ctx:
+            for _ in range(frames // per_call):
+                ctx.render(per_call, True)
+            img = ctx.readback(W, H)
+            cnt = ctx.counters()
+        assert_bitwise(img, ref, f"idle {idle_us} us, {per_call} per call: {cnt['server_launches']} lifetimes, "
+                                 f"{cnt['server_refused']} posts refused")
+        assert cnt["server_frames"] == frames and cnt["frames_lost"] == 0 and cnt["paths"] == rc["paths"], cnt
+        assert cnt["server_launches"] > 1, cnt  # the server closed between posts at least once
+        print(f"idle {idle_us} us, {per_call} per call: {cnt['server_launches']} lifetimes, "
+              f"{cnt['server_refused']} refused posts")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tiling", [None, (1, 2)])
+def test_gpu_server_lost_frame_leaves_the_accumulator(gpu, tiling):
+    """A frame whose gate gives up (HG_OPT_SERVER_GATE_US 0: the gate of a 1080p C3 frame, launched microseconds after
+    its post, finds the frame unfinished) is lost: its blend and every later one are skipped, so the accumulator keeps
+    the image of the frames before it; hg_render refuses, and every readback (single-rank, a rank's tiles, the display
+    ring) hands out that image with HG_E_FRAME_LOST, until hg_clear_accumulation starts a valid accumulation again."""
+    cfg = scenes.CONFIGS["C3"]
+    packed, params, cube = _sized("C3", cfg.width, cfg.height)
+    W, H = cfg.width, cfg.height
+    want3 = gpu_render(packed, params, 3, True, cube, tiling=tiling)[0]
+    ctx, _, _ = _ctx(packed, params, cube, tiling=tiling)
+    with ctx:
+        for _ in range(3):
+            ctx.render(1, True)
+        before = np.full((H, W, 4), np.nan, np.float32)  # (with tiling, other ranks' pixels stay untouched)
+        ctx.readback(W, H, before)
+        assert_bitwise(before, want3, "3 frames before the loss")
+        ctx.set_option(abi.HG_OPT_SERVER_GATE_US, 0)
+        try:
+            for _ in range(2):
+                ctx.render(1, True)
+        except abi.HalogenError as e:  # (the second call may already see the first frame's loss)
+            assert e.rc == abi.HG_E_FRAME_LOST, e
+        img = np.full((H, W, 4), np.nan, np.float32)
+        with pytest.raises(abi.HalogenError) as e:
+            ctx.readback(W, H, img)
+        assert e.value.rc == abi.HG_E_FRAME_LOST, e.value
+        assert_bitwise(img, before, "the accumulator after a lost frame")
+        with pytest.raises(abi.HalogenError) as e:
+            ctx.render(1, True)
+        assert e.value.rc == abi.HG_E_FRAME_LOST
+        ctx.readback_begin(abi.HG_DISPLAY_RGBA32F)
+        with pytest.raises(abi.HalogenError) as e:
+            ctx.readback_end(W, H)
+        assert e.value.rc == abi.HG_E_FRAME_LOST
+        cnt = ctx.counters()
+        assert cnt["frames_lost"] >= 1, cnt
+        # a clear starts a valid accumulation: the same 3 frames again (FrameCount 1) equal the batched image
+        ctx.set_option(abi.HG_OPT_SERVER_GATE_US, -1)
+        ctx.clear_accumulation()
+        ctx.set_params(params)
+        for _ in range(3):
+            ctx.render(1, True)
+        again = np.full((H, W, 4), np.nan, np.float32)
+        ctx.readback(W, H, again)
+    assert_bitwise(again, want3, "3 frames after the clear")
