@@ -3,7 +3,9 @@
 871,200-triangle dragon Cornell box (config C3), on N GPUs of one node.
 
   python bench.py [--gpus N --steps K --warmup W] [--config C3]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N; run without
+  a launcher, `python bench.py --gpus N` starts that launcher itself as a child process, before anything touches a GPU,
+  and relays rank 0's line and the exit status)
 
 A STEP is one complete C3 image PER GPU: 64 progressive frames of 1 spp (the reference's unit of work is one
 frame = one HalogenCompute dispatch + one accumulation blit, RP:324-347; C3 accumulates 64 of them) over the
@@ -31,6 +33,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -38,6 +42,51 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parent
+
+
+def gpus_requested(argv) -> int:
+    """--gpus N (either form) of a command line, 1 when absent or malformed."""
+    for i, a in enumerate(argv):
+        try:
+            if a == "--gpus" and i + 1 < len(argv):
+                return int(argv[i + 1])
+            if a.startswith("--gpus="):
+                return int(a.split("=", 1)[1])
+        except ValueError:
+            return 1
+    return 1
+
+
+def self_launch_command(argv, n: int, port: int) -> list:
+    """The launcher the driver would have used: one process per GPU (torch.distributed.run, rendezvous on 127.0.0.1),
+    each running this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def self_launch(argv) -> int | None:
+    """`bench.py --gpus N` (N > 1) started without a launcher (no WORLD_SIZE): start the N ranks as a child launcher and
+    return its exit status (non-zero if any rank failed); rank 0 prints the one JSON line, on the inherited stdout.  Runs
+    before halogen is imported, so this process never initialises a GPU (the children each open their own).  None: this
+    process is a rank (or N = 1) and runs the bench itself."""
+    if "WORLD_SIZE" in os.environ:
+        return None
+    n = gpus_requested(argv)
+    if n <= 1:
+        return None
+    with socket.socket() as sk:  # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between the ranks' processes)
+    return subprocess.run(self_launch_command(argv, n, port), env=env).returncode
+
+
+if __name__ == "__main__":
+    _rc = self_launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
 sys.path.insert(0, str(ROOT / "halogen-pathtracer_amd"))
 
 from halogen import abi  # noqa: E402
@@ -442,6 +491,57 @@ def strong_scaling_measurement(ctx, params, W, H, fps: int, steps: int, world: i
     return res
 
 
+def compact_summary(result: dict) -> dict:
+    """The operating points in a few hundred bytes, the last key of the line (the driver keeps the line's last 8 KB):
+    the headline, the per-frame points as fractions of it, the camera-move frame, the framed and SAH views, the strong
+    leg and the roofline fraction."""
+    def r(x, nd=3):
+        return None if x is None else round(float(x), nd)
+
+    pf = result.get("per_frame") or {}
+    strict = pf.get("strict") or {}
+    disp = (pf.get("with_display_readback") or {}).get("r11g11b10f") or {}
+    cam = result.get("camera_move") or {}
+    strong = result.get("strong_scaling") or {}
+    roof = result.get("roofline") or {}
+    behind = {"at_once": "sync", "one_behind": "pipelined", "three_behind": "pipelined_depth4",
+              "seven_behind": "pipelined_depth8_side", "fifteen_behind": "pipelined_depth16"}
+    return {
+        "value": r(result.get("value"), 1),
+        "primary_miss_frac": r(result.get("primary_miss_frac")),
+        "roofline_frac": r(roof.get("frac")),
+        "per_frame": {
+            "coalesced": {"frac_of_batched": r(pf.get("frac_of_batched"))},
+            "strict": {"value": r(strict.get("value"), 1), "frac_of_batched": r(strict.get("frac_of_batched")),
+                       "server_launches": strict.get("server_launches")},
+            "per_launch": {"frac_of_batched": r((strict.get("per_launch") or {}).get("frac_of_batched"))},
+            "display_r11g11b10f": {k: r((disp.get(m) or {}).get("frac_of_batched")) for k, m in behind.items()},
+        } if pf else None,
+        "camera_move": {"value": r(cam.get("value"), 1), "frac_of_batched": r(cam.get("value") / result["value"])
+                        if cam.get("value") else None, "upload_share": r(cam.get("upload_share"), 4)} if cam else None,
+        "framed": r((result.get("framed") or {}).get("value"), 1),
+        "fast_bvh": r((result.get("fast_bvh") or {}).get("value"), 1),
+        "strong": {"n_ranks": strong.get("n_ranks"), "value": r(strong.get("value"), 1),
+                   "per_gpu_frac_of_weak": r(strong.get("per_gpu_frac_of_weak"))} if strong else None,
+    }
+
+
+def split_detail(result: dict, path: str) -> None:
+    """The per-format display tables go to `path` (JSON), the line keeps the reference's display format
+    (R11G11B10F) and the bit-identity checks."""
+    pf = result.get("per_frame")
+    if not pf or not pf.get("with_display_readback"):
+        return
+    full = pf["with_display_readback"]
+    pf["with_display_readback"] = {k: v for k, v in full.items() if k not in ("rgba32f", "rgba16f")}
+    pf["with_display_readback"]["other_formats"] = path
+    try:
+        Path(path).parent.mkdir(parents=True, exist_ok=True)
+        Path(path).write_text(json.dumps({"with_display_readback": full, "config": result.get("config")}, indent=1))
+    except OSError as e:
+        pf["with_display_readback"]["other_formats"] = f"not written: {e}"
+
+
 def committed_counters(config: str, W: int, H: int, frames_per_launch: int, kernel_symbol: str) -> dict:
     """The committed PMC figures of this workload's production kernel (tools/summarize_profile.py):
     profiles/pmc_traffic_<config>.json, or profiles/pmc_traffic.json (the headline config's), when they match the
@@ -641,8 +741,14 @@ def main():
                          "or hg_build_blas_sah (NOT the reference's hierarchy; A/B and the fast_bvh leg)")
     ap.add_argument("--sah-leaf", type=int, default=2, help="--bvh sah: largest leaf the SAH build makes by size alone")
     ap.add_argument("--no-fast-bvh", action="store_true", help="skip the fast_bvh leg (C3 on an SAH BLAS)")
+    ap.add_argument("--queue-fill", type=int, default=-1, help="HG_OPT_QUEUE_FILL (0 off, k rounds); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--no-strong", action="store_true", help="N > 1 / --emulate-ranks: skip the strong-scaling leg")
+    ap.add_argument("--dist-probe", action="store_true",
+                    help="launcher check, no GPU: every rank joins the process group, all-reduces its rank, rank 0 prints "
+                         "one JSON line (tests/test_bench_launch.py)")
+    ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                    help="the per-format display tables and other bulky legs (the line keeps a compact summary)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of one rank's share at N ranks (tiles t %% N == 0, N*fps frames); "
                          "reports that rank's own Mpaths/s, not a contract line")
@@ -655,8 +761,27 @@ def main():
     device = int(os.environ.get("HALOGEN_BENCH_DEVICE", local_rank))  # rehearsal: every rank on one GPU
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+            raise SystemExit(f"--gpus {args.gpus}: run bench.py as a script (it starts its {args.gpus} ranks itself) "
+                             f"or under torch.distributed.run with {args.gpus} processes")
     dist = None
+    if args.dist_probe:  # the launcher's check (no GPU, gloo): the ranks join, agree, and rank 0 prints one line
+        import torch
+        import torch.distributed as dist_mod
+
+        if world > 1:
+            dist_mod.init_process_group("gloo")
+        if os.environ.get("HALOGEN_BENCH_PROBE_FAIL_RANK") == str(rank):  # (the test of a failing rank's exit status)
+            raise SystemExit(3)
+        t = torch.tensor([float(rank)])
+        if world > 1:
+            dist_mod.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"dist_probe": True, "world": world, "rank_sum": int(t.item()),
+                              "local_ranks_device": device}), flush=True)
+        if world > 1:
+            dist_mod.barrier()
+            dist_mod.destroy_process_group()
+        return
     if world > 1:
         import torch
         import torch.distributed as dist_mod
@@ -706,6 +831,8 @@ def main():
         ctx.set_option(abi.HG_OPT_SERVER, args.server)
     if args.descent_t >= -1:
         ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
+    if args.queue_fill >= 0:
+        ctx.set_option(abi.HG_OPT_QUEUE_FILL, args.queue_fill)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:
@@ -1067,6 +1194,12 @@ def main():
             threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
                                  else (os.cpu_count() or 1)))
             result["cpu_baseline"] = cpu_baseline(packed, params, cube, W, H, args.cpu_seconds, threads)
+        if strong and strong.get("value"):
+            # the strong leg's rate per GPU against this line's weak rate per GPU (N ranks: both totals over N GPUs;
+            # --emulate-ranks: both rank 0's share on its one GPU, so the ratio is the same quantity)
+            strong["per_gpu_frac_of_weak"] = strong["value"] / result["value"]
+        split_detail(result, args.detail_out)
+        result["summary"] = compact_summary(result)
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.close()

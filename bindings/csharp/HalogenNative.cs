@@ -79,7 +79,8 @@ public static class HalogenNative
     public const int HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
                      HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
-                     HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17;
+                     HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17,
+                     HG_OPT_QUEUE_FILL = 18;
     public const int HG_READBACK_MAX = 16;
     // display formats of hg_readback_begin_format / hg_comm_readback_begin: 16 / 8 / 4 bytes per pixel; R11G11B10F is
     // the URP HDR camera target the reference blits into (GraphicsFormat.B10G11R11_UFloatPack32: R in bits 0-10)

@@ -133,6 +133,7 @@ struct hg_ctx {
     int32_t lane_pick = HG_LANE_PICK;  // HG_OPT_LANE_PICK: 1-frame chunks on the first idle trace stream (1) or in turn (0)
     int32_t descent_t = -1;   // < 0: automatic from the BLAS depth
     int32_t tile_order_on = HG_TILE_ORDER;  // HG_OPT_TILE_ORDER
+    int32_t queue_fill = HG_QUEUE_FILL;     // HG_OPT_QUEUE_FILL
     // Render coalescing (HG_OPT_COALESCE): hg_render is asynchronous, so consecutive calls with the same parameters are
     // held and launched as one multi-frame launch once `coalesce` frames are pending, or as soon as anything reads or
     // changes the context's state (every other entry point flushes first: hg_ctx_flush).  Same frames, same order,

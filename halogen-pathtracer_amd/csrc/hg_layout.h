@@ -131,6 +131,9 @@
 #define HG_LANE_PICK 1  // default HG_OPT_LANE_PICK (display one frame behind +5 %, strict -0.5 %: sweep_r04_depth)
 #endif
 #define HG_WAVE_UNITS_LIMIT 4  // HG_OPT_WAVE_UNITS range (the units' tiles sit in scalar registers)
+#ifndef HG_QUEUE_FILL
+#define HG_QUEUE_FILL 4  // default HG_OPT_QUEUE_FILL: streaming launches whose tiles give fewer rounds of wave slots run the queue form
+#endif
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif

@@ -510,7 +510,6 @@ void hg_destroy(hg_ctx* c) {
                                           hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
             hipStreamSynchronize(c->stream) == hipSuccess)
             sv_trace("destroy: server waves out %llu of %llu", w[0] & 0xFFFFFFFFull, w[0] >> 32);
-        sv_trace("destroy: device synchronize %s", hipGetErrorString(hipDeviceSynchronize()));
     }
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     sv_trace("destroy: context stream idle");
@@ -519,31 +518,60 @@ void hg_destroy(hg_ctx* c) {
     for (DevBuf* b : {&c->spheres, &c->meshes, &c->materials, &c->nodes, &c->leaves, &c->tris, &c->normals, &c->cube,
                       &c->acc, &c->counters_dev, &c->spill, &c->lost})
         release(*b);
-    for (hg_ctx::TraceLane& L : c->lanes) {
-        for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.order_scratch, &L.queue})
-            release(*b);
-        if (L.traced) (void)hipEventDestroy(L.traced);
-        if (L.blended) (void)hipEventDestroy(L.blended);
-        if (L.stream) (void)hipStreamDestroy(L.stream);
+    auto destroy_lanes = [c] {
+        for (hg_ctx::TraceLane& L : c->lanes) {
+            for (DevBuf* b : {&L.frame_color, &L.spill, &L.tile_cost, &L.tile_order, &L.order_scratch, &L.queue})
+                release(*b);
+            if (L.traced) (void)hipEventDestroy(L.traced);
+            if (L.blended) (void)hipEventDestroy(L.blended);
+            sv_trace("destroy: lane stream %p", static_cast<void*>(L.stream));
+            if (L.stream) (void)hipStreamDestroy(L.stream);
+        }
+        sv_trace("destroy: trace streams destroyed");
+    };
+    // (analysis builds, HG_DIAG_TEARDOWN: HALOGEN_DIAG_TEARDOWN=server_first[,bufs_last][,host_last][,events_last]
+    // destroys the server's stream before the trace streams, the order that hung in round 5, and defers the named
+    // server resources past every stream destroy: tools/gpu_teardown.sh)
+    bool server_first = false, bufs_last = false, host_last = false, events_last = false;
+#if HG_DIAG_TEARDOWN
+    if (const char* td = std::getenv("HALOGEN_DIAG_TEARDOWN")) {
+        server_first = std::strstr(td, "server_first") != nullptr;
+        bufs_last = std::strstr(td, "bufs_last") != nullptr;
+        host_last = std::strstr(td, "host_last") != nullptr;
+        events_last = std::strstr(td, "events_last") != nullptr;
     }
-    sv_trace("destroy: trace streams destroyed");
-    // The server's stream after the trace streams: destroyed before them, the next hipStreamDestroy of a plain trace
-    // stream hung (HIP 7.2 on the MI355X box, every time after a 200-frame server run with one frame per call; streams
-    // idle and every server wave out, per HALOGEN_SERVER_TRACE)
-    {
-        hg_ctx::Server& S = c->sv;
-        if (S.stream) (void)hipStreamSynchronize(S.stream);
-        sv_trace("destroy: every stream idle");
+#endif
+    hg_ctx::Server& S = c->sv;
+    auto server_bufs = [&S] {
         for (DevBuf* b : {&S.ctl, &S.done, &S.ring, &S.spill, &S.tile_cost, &S.tile_order, &S.order_scratch}) release(*b);
         sv_trace("destroy: server buffers freed");
+    };
+    auto server_events = [&S] {
         for (hipEvent_t& e : S.blended)
             if (e) (void)hipEventDestroy(e);
         sv_trace("destroy: server events destroyed");
+    };
+    auto server_host = [&S] {
         if (S.host) (void)hipHostFree(S.host);
         sv_trace("destroy: server host word freed");
+    };
+    auto destroy_server = [&] {
+        if (S.stream) (void)hipStreamSynchronize(S.stream);
+        sv_trace("destroy: server stream idle");
+        if (!bufs_last) server_bufs();
+        if (!events_last) server_events();
+        if (!host_last) server_host();
         if (S.stream) (void)hipStreamDestroy(S.stream);
         sv_trace("destroy: server stream destroyed");
-    }
+    };
+    // The server's stream after the trace streams: destroyed before them, the next hipStreamDestroy of a plain trace
+    // stream hung in round 5 (DESIGN.md section 4.7 has what the analysis build found)
+    if (server_first) destroy_server();
+    destroy_lanes();
+    if (!server_first) destroy_server();
+    if (bufs_last) server_bufs();
+    if (events_last) server_events();
+    if (host_last) server_host();
     if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
     release(c->image);
     for (int k = 0; k < HG_READBACK_MAX; ++k) {
@@ -1376,8 +1404,13 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 kc.frame_split = std::min(split, kc.n_frames);
                 kc.frame_color = static_cast<float4*>(L.frame_color.p);
                 kc.spill = spill_bytes ? static_cast<uint32_t*>(L.spill.p) : nullptr;
-                // the persistent work-queue form for launches of few frames (the reference's one dispatch per frame)
-                kc.queue = stream_k && kc.n_frames <= HG_QUEUE_MAX_FRAMES ? static_cast<uint32_t*>(L.queue.p) : nullptr;
+                // the persistent work-queue form for launches of few frames (the reference's one dispatch per frame),
+                // and for a share of the tiles too small to fill the GPU with per-tile waves (a rank's 1/N of the image
+                // at N GPUs, HG_OPT_QUEUE_FILL): persistent waves pull (tile, frame chunk) units, so a wave's lanes
+                // drain once per launch, not once per short wave
+                const bool fill = c->queue_fill > 0 && tiles < int64_t(c->queue_fill) * int64_t(slots);
+                kc.queue = stream_k && (kc.n_frames <= HG_QUEUE_MAX_FRAMES || fill) ? static_cast<uint32_t*>(L.queue.p)
+                                                                                     : nullptr;
                 // Persistent waves of a queue launch.  A launch's end costs each of its waves the time its last paths
                 // take, with its lanes draining; fewer, longer-lived waves pay that less often.  So while two or more
                 // other traces are in flight (which fill the slots), a launch takes slots / min(HG_QUEUE_WAVES_DIV,
@@ -1907,6 +1940,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_SERVER:
             if (value < 0 || value > 2) return fail(c, HG_E_INVALID, "HG_OPT_SERVER %d: expected 0, 1 or 2", value);
             c->server_on = value;
+            return HG_OK;
+        case HG_OPT_QUEUE_FILL:
+            if (value < 0 || value > 64) return fail(c, HG_E_INVALID, "queue fill threshold must be 0 (off)..64 rounds");
+            c->queue_fill = value;
             return HG_OK;
         case HG_OPT_SERVER_IDLE_US:
             if (value < 0 || value > 40000000) return fail(c, HG_E_INVALID, "server idle time must be 0..40000000 us");

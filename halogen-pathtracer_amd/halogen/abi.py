@@ -107,6 +107,7 @@ HG_OPT_LANE_PICK = 14
 HG_OPT_SERVER = 15
 HG_OPT_SERVER_IDLE_US = 16
 HG_OPT_SERVER_GATE_US = 17
+HG_OPT_QUEUE_FILL = 18
 HG_E_INVALID, HG_E_HIP, HG_E_NOMEM, HG_E_NOSCENE, HG_E_NOTARGET, HG_E_UNSUPPORTED, HG_E_COMM = -1, -2, -3, -4, -5, -6, -7
 HG_E_FRAME_LOST = -8
 HG_READBACK_MAX = 16

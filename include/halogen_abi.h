@@ -239,7 +239,11 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
 enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING = 4, HG_OPT_REFILL = 5,
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
        HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
-       HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17 };
+       HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17,
+       HG_OPT_QUEUE_FILL = 18 };
+/* HG_OPT_QUEUE_FILL (default 4): a streaming launch of more than 8 frames whose tiles number fewer than this many rounds
+ *   of the GPU's wave slots (a rank's 1/N share of the image at N GPUs: strong scaling) runs the persistent work-queue
+ *   form, its waves pulling (tile, frame chunk) units instead of one short wave per chunk.  0 = never.  Same images. */
 /* HG_OPT_SERVER (default 1): hg_render calls of at most 8 accumulating frames on the streaming kernel (the reference's
  *   one dispatch per frame, RP:327) post their frames to a render server — persistent trace waves that outlive the call
  *   and take each posted frame's (tile, frame) units as soon as lanes free up, so one frame's last paths overlap the

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--per-call", default="1,2,8")
     ap.add_argument("--check-every", type=int, default=0, help="read back and compare every k frames (0: at the end)")
     ap.add_argument("--tilings", default="none,2/3")
+    ap.add_argument("--server", type=int, default=2, help="HG_OPT_SERVER (2: every qualifying call)")
     a = ap.parse_args()
     Path(a.log).parent.mkdir(parents=True, exist_ok=True)
     out = open(a.log, "w")
@@ -62,6 +63,7 @@ def main():
         for per_call in (int(v) for v in a.per_call.split(",")):
             ctx = abi.Context(0)
             ctx.set_option(abi.HG_OPT_COALESCE, 1)
+            ctx.set_option(abi.HG_OPT_SERVER, a.server)
             ctx.upload_scene(packed)
             if cube is not None:
                 ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
