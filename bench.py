@@ -282,7 +282,9 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
         res = {"bytes_per_frame": W * H * abi.DISPLAY_BPP[fmt]}
         for mode, depth, side in (("sync", 1, 0), ("pipelined", 2, 0), ("pipelined_depth4", 4, 0),
                                   ("pipelined_side", 2, 1), ("pipelined_depth4_side", 4, 1),
-                                  ("pipelined_depth8_side", 8, 1), ("pipelined_depth16", 16, 0)):
+                                  ("pipelined_depth8_side", 8, 1), ("pipelined_depth16", 16, 0),
+                                  ("sync_zero_copy", 1, 2), ("pipelined_zero_copy", 2, 2),
+                                  ("pipelined_depth4_zero_copy", 4, 2)):
             fresh()
             ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
             ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)
@@ -303,7 +305,7 @@ def per_frame_measurement(ctx, params, W, H, frames: int, reps: int, batched_val
             v = paths / dt_d / 1e6
             res[mode] = {"value": v, "unit": "Mpaths/s", "ms_per_frame": dt_d * 1e3 / frames,
                          "frac_of_batched": v / batched_value, "frames_behind": depth - 1,
-                         "copy_stream": "side" if side else "context"}
+                         "copy_stream": {0: "context", 1: "side", 2: "none (zero copy)"}[side]}
         display[fmt_name] = res
     ctx.set_option(abi.HG_OPT_READBACK_DEPTH, 2)
     ctx.set_option(abi.HG_OPT_READBACK_STREAM, 0)
@@ -742,6 +744,7 @@ def main():
     ap.add_argument("--sah-leaf", type=int, default=2, help="--bvh sah: largest leaf the SAH build makes by size alone")
     ap.add_argument("--no-fast-bvh", action="store_true", help="skip the fast_bvh leg (C3 on an SAH BLAS)")
     ap.add_argument("--queue-fill", type=int, default=-1, help="HG_OPT_QUEUE_FILL (0 off, k rounds); -1: default")
+    ap.add_argument("--server-ahead", type=int, default=-1, help="HG_OPT_SERVER_AHEAD (frames traced ahead); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--no-strong", action="store_true", help="N > 1 / --emulate-ranks: skip the strong-scaling leg")
     ap.add_argument("--dist-probe", action="store_true",
@@ -833,6 +836,8 @@ def main():
         ctx.set_option(abi.HG_OPT_DESCENT_T, args.descent_t)
     if args.queue_fill >= 0:
         ctx.set_option(abi.HG_OPT_QUEUE_FILL, args.queue_fill)
+    if args.server_ahead >= 0:
+        ctx.set_option(abi.HG_OPT_SERVER_AHEAD, args.server_ahead)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:
@@ -875,6 +880,7 @@ def main():
     frames_per_step = (emu or world) * args.frames_per_step  # per-GPU work fixed: image frame-equivalents per GPU
     if args.per_frame_only:  # profiling aid (tools/profile.sh): one warm-up step of the same launches, then steps x frames x hg_render(1)
         ctx.set_option(abi.HG_OPT_COALESCE, args.coalesce)
+        ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # (the per-frame legs run the production kernels)
         depth = 1 if args.display == "sync" else args.readback_depth
         ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
         ctx.set_option(abi.HG_OPT_READBACK_STREAM, args.readback_stream)
@@ -913,6 +919,7 @@ def main():
         print(json.dumps({"per_frame_only": True, "value": W * H * frames_per_step * args.steps / dt / 1e6,
                           "unit": "Mpaths/s", "launches": c["launches"], "ms_per_step": dt * 1e3 / args.steps,
                           "server_launches": c["server_launches"], "server_frames": c["server_frames"],
+                          "server_ahead": c["server_ahead"],
                           "device_ms_per_frame": c["kernel_ms"] / max(c["launches"], 1),
                           "host_ms_per_call": {k: v * 1e3 / n_calls for k, v in host.items()}}), flush=True)
         ctx.close()

@@ -71,6 +71,7 @@ public static class HalogenNative
         public ulong server_frames;
         public ulong server_refused;
         public ulong frames_lost;
+        public ulong server_ahead;
     }
 
     public const int HG_OK = 0;
@@ -80,7 +81,7 @@ public static class HalogenNative
                      HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
                      HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
                      HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17,
-                     HG_OPT_QUEUE_FILL = 18;
+                     HG_OPT_QUEUE_FILL = 18, HG_OPT_SERVER_AHEAD = 19;
     public const int HG_READBACK_MAX = 16;
     // display formats of hg_readback_begin_format / hg_comm_readback_begin: 16 / 8 / 4 bytes per pixel; R11G11B10F is
     // the URP HDR camera target the reference blits into (GraphicsFormat.B10G11R11_UFloatPack32: R in bits 0-10)

@@ -135,6 +135,9 @@ public class HalogenRenderPass : ScriptableRenderPass
         {
             int rc = HalogenNative.hg_create(d, out contexts[d]);
             if (rc != HalogenNative.HG_OK) throw new Exception($"hg_create({d}) failed ({rc}): no usable MI355X device");
+            // the pass never reads the work counters (the reference has none); off, the render server may trace the
+            // next frames of an unchanged camera ahead of the calls (HG_OPT_SERVER_AHEAD)
+            Check(HalogenNative.hg_set_option(contexts[d], HalogenNative.HG_OPT_COUNTERS, 0), "hg_set_option(HG_OPT_COUNTERS)");
         }
 
         string fmt = (Environment.GetEnvironmentVariable("HALOGEN_DISPLAY_FORMAT") ?? "r11g11b10f").ToLowerInvariant();

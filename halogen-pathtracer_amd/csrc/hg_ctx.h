@@ -90,6 +90,7 @@ struct hg_ctx {
         bool tile_cost_valid = false;
         unsigned long long* host = nullptr;  // pinned, coherent: the host words HG_SV_HOST_* (hg_layout.h)
         uint32_t ring_n = 0, posted = 0, cap = 0;
+        uint32_t committed = 0;  // frames the host asked for (gate + blend queued); posted - committed were posted ahead
         uint32_t uses[HG_SV_RING] = {};     // frames posted to each ring slot in this lifetime
         hipEvent_t blended[HG_SV_RING] = {};  // after the blend of each ring slot's last frame
         bool blend_valid[HG_SV_RING] = {};
@@ -105,6 +106,13 @@ struct hg_ctx {
     int32_t server_on = 1;  // HG_OPT_SERVER
     uint64_t server_launches = 0, server_frames = 0;
     uint64_t server_refused = 0;  // posts that met a closing server (the close handshake), re-posted to a new one
+    // HG_OPT_SERVER_AHEAD: frames the server traces ahead of the host's calls (counters off), and the call chain that
+    // engages the server without a host running ahead: consecutive accumulating calls with the same parameters, each
+    // continuing the last one's FrameCount
+    int32_t sv_ahead = HG_SV_AHEAD;
+    uint64_t server_ahead_posts = 0;
+    hg_params chain_params{};
+    int32_t chain_next = 0, chain_len = 0;
     // Lost frames (a server frame's gate gave up, hg_server_gate): the gate raises `lost` (uncached device memory), and
     // every later blend into the accumulator is skipped; the host marks the accumulator invalid (acc_lost) when it reads
     // the gate's host word and the frame belongs to the current accumulation (acc_epoch: advanced by every clear,
@@ -148,6 +156,7 @@ struct hg_ctx {
     size_t image_host_cap[HG_READBACK_MAX] = {};    // allocated bytes
     size_t image_host_bytes[HG_READBACK_MAX] = {};  // bytes of the readback it holds
     int32_t image_host_format[HG_READBACK_MAX] = {};
+    bool image_host_mapped[HG_READBACK_MAX] = {};  // allocated mapped + fine-grained (HG_OPT_READBACK_STREAM 2)
     hipEvent_t image_copied[HG_READBACK_MAX] = {};
     int rb_depth = 2;                 // HG_OPT_READBACK_DEPTH: readbacks that may be outstanding
     int rb_side = HG_READBACK_SIDE;   // HG_OPT_READBACK_STREAM: copies on rb_stream from per-slot device images

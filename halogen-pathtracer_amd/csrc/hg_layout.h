@@ -75,6 +75,9 @@
 // waves issue first) and 0 while shading (C3 2,097 -> 2,111, tools/sweeps/sweep67-68.txt); the regenerating kernel's
 // at 1 during get_ray_intersection (C2 +1 %, C5 +2 %, tools/sweeps/sweep69.txt).
 #define HG_TRAVERSE_PRIO 1
+#ifndef HG_DRAIN_PRIO
+#define HG_DRAIN_PRIO 0  // queue launches: waves whose queue ran dry issue at priority 3 / 2 (traversal / shading)
+#endif
 #ifndef HG_TILE_ORDER
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif
@@ -132,8 +135,13 @@
 #endif
 #define HG_WAVE_UNITS_LIMIT 4  // HG_OPT_WAVE_UNITS range (the units' tiles sit in scalar registers)
 #ifndef HG_QUEUE_FILL
-#define HG_QUEUE_FILL 4  // default HG_OPT_QUEUE_FILL: streaming launches whose tiles give fewer rounds of wave slots run the queue form
+// default HG_OPT_QUEUE_FILL: streaming launches of more than HG_QUEUE_MAX_FRAMES frames whose tiles give fewer rounds of
+// the GPU's wave slots than this run the queue form (a rank's share at N = 8, 1080p: 0.79 rounds).  The queue form
+// costs 13 % per item against per-tile waves (C3 at N = 1: 3,042 vs 3,491 Mpaths/s; same instruction counts), so it
+// pays only below one round (emulated N = 4 share, 1.58 rounds: 2,842 vs 3,114)
+#define HG_QUEUE_FILL 1
 #endif
+#define HG_QUEUE_FILL_UNITS 24  // queue-form shares: (tile, frame chunk) units per wave slot
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif
@@ -187,6 +195,9 @@
 #define HG_SV_HOST_CLOSED 3
 #define HG_SV_CLOSED (1ull << 33)
 #define HG_SV_LOST (1ull << 32)
+#ifndef HG_SV_AHEAD
+#define HG_SV_AHEAD 4  // default HG_OPT_SERVER_AHEAD: frames the render server traces ahead of the host's calls (4 and 8 measured equal)
+#endif
 #define HG_SV_IDLE_US 200000  // default HG_OPT_SERVER_IDLE_US: the server closes after this long with nothing posted
 #ifndef HG_REGEN_ITEMS
 #define HG_REGEN_ITEMS 1  // regenerating kernel: (pixel, frame) item scheduling (0: the A/B build of make noitems)

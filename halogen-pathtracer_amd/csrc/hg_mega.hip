@@ -804,6 +804,10 @@ __shared__ QueueUnit hg_qu[2];
 __shared__ uint32_t hg_q_cur;  // the unit whose items come first
 __shared__ uint32_t hg_q_dry;  // the queue has no unit left
 __shared__ uint32_t hg_q_empty;  // the queue has no unit left and both units are spent (the wave's lanes retire)
+// (kQueue launches, not the server) a lane's take reached past the first unit (or found both spent): the loop top must
+// refill.  Raised by the taking lanes, cleared by the refill; the loop top reads this one word instead of running the
+// refill (lane 0's reads of the item count, the current unit and its end) on every trace / shade round.
+__shared__ uint32_t hg_q_need;
 
 // Pull the next unit of the queue into hg_qu[slot], its items numbered from `base` (one lane).  When the queue is dry
 // the unit is empty (end = base) and hg_q_dry is set.  Attributes the wave clock since the previous pull to the
@@ -874,6 +878,7 @@ __device__ __forceinline__ bool queue_item(uint32_t k, uint32_t& slot, uint32_t&
     const uint32_t a = __builtin_amdgcn_readfirstlane(lds_get(hg_q_cur));
     const uint32_t a_end = __builtin_amdgcn_readfirstlane(lds_get(hg_qu[a].end));
     const uint32_t b_end = __builtin_amdgcn_readfirstlane(lds_get(hg_qu[a ^ 1u].end));
+    if (k >= a_end) lds_put(hg_q_need, 1u);  // the first unit is spent (the server's loop top refills every round)
     if (k >= b_end && k >= a_end) return false;
     QueueUnit& q = hg_qu[k < a_end ? a : a ^ 1u];
     const uint32_t base = lds_get(q.base);
@@ -1020,7 +1025,9 @@ __device__ uint32_t sv_view(const HgKernelParams& kp) {
     uint32_t v = lds_get(hg_sv.view);
     const unsigned long long m = sv_sload(sv_word64(kp, HG_SV_MIRROR_WORD + 32u * (blockIdx.x % HG_SV_MIRRORS)));
     const uint32_t u = sv_units(m);
-    if (u > v) {
+    // a post word with the stop flag is final: its count may be below the frames posted ahead of the host's calls
+    // (hg_runtime.hip server_speculate), which are abandoned (the units already pulled are traced)
+    if (u > v || ((m & HG_SV_STOP) && u != v)) {
         v = u;
         lds_put(hg_sv.view, v);
     }
@@ -1243,6 +1250,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
             }
             lds_put(hg_q_cur, 0u);
             lds_put(hg_q_dry, 0u);
+            lds_put(hg_q_need, 1u);  // (both units empty: the first loop top pulls two)
             hg_wave_cost[threadIdx.x >> 6] = nullptr;
             if constexpr (kServer) sv_init(kp);
         }
@@ -1328,9 +1336,14 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 }
             } else if (kQueue && !dry) {
                 wave_lds_sync();
-                if (lane == 0u) lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
-                wave_lds_sync();
-                dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
+                if (__builtin_amdgcn_readfirstlane(lds_get(hg_q_need)) != 0u) {  // (an idle lane implies a take past it)
+                    if (lane == 0u) {
+                        lds_put(hg_q_need, 0u);
+                        lds_put(hg_q_empty, queue_refill(kp, n_units, split) ? 1u : 0u);
+                    }
+                    wave_lds_sync();
+                    dry = __builtin_amdgcn_readfirstlane(lds_get(hg_q_empty)) != 0u;
+                }
                 if (!work && !dry) {
                     work = true;
                     bounce = kFreshLane;
@@ -1352,7 +1365,10 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 cyc_trav += t;
                 cyc_shade -= t;
             }
-            __builtin_amdgcn_s_setprio(0);
+            // (HG_DRAIN_PRIO, queue launches: a wave whose queue ran dry holds the launch's last paths; it issues ahead of
+            // the next launch's waves, so the frame completes sooner: the latency a per-frame display waits on)
+            if (HG_DRAIN_PRIO && kQueue && !kServer && dry) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
             // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
             // (rays that finish at once — everything culled — shade again in this loop while at least
             // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
@@ -1461,7 +1477,8 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
                 }
             }
-            __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
+            if (HG_DRAIN_PRIO && kQueue && !kServer && dry) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
             if (kCounters) cyc_shade += wave_clock();
         }
         if constexpr (!kServer) {

@@ -361,9 +361,11 @@ int reset_lost(hg_ctx* c) {
 int server_stop(hg_ctx* c) {
     hg_ctx::Server& S = c->sv;
     if (!S.running) return HG_OK;
-    __atomic_store_n(&S.host[0], static_cast<unsigned long long>(S.posted) | HG_SV_STOP, __ATOMIC_SEQ_CST);
+    // the stop word carries the frames the host asked for: frames posted ahead of the calls (server_speculate) and not
+    // yet claimed are abandoned (the waves' view drops to it, hg_mega.hip sv_view)
+    __atomic_store_n(&S.host[HG_SV_HOST_POST], static_cast<unsigned long long>(S.committed) | HG_SV_STOP, __ATOMIC_SEQ_CST);
     const double t0 = host_seconds();
-    sv_trace("stop: %u frames posted", S.posted);
+    sv_trace("stop: %u frames committed, %u posted", S.committed, S.posted);
     hipError_t q;
     while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
         if (host_seconds() - t0 > 60.0) {
@@ -941,7 +943,7 @@ bool server_continues(hg_ctx* c, int32_t fc) {
     if (!S.running) return false;
     hg_params p = c->params;
     p.frameCount = S.params.frameCount;
-    if (std::memcmp(&p, &S.params, sizeof p) != 0 || int64_t(fc) != int64_t(S.params.frameCount) + int64_t(S.posted) ||
+    if (std::memcmp(&p, &S.params, sizeof p) != 0 || int64_t(fc) != int64_t(S.params.frameCount) + int64_t(S.committed) ||
         S.kernel_variant != c->kernel || S.descent_t != c->descent_t || S.posted >= S.cap ||
         __atomic_load_n(&S.host[HG_SV_HOST_CLOSING], __ATOMIC_SEQ_CST) != 0ull)
         return false;
@@ -1060,6 +1062,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     S.running = true;
     S.ring_n = ring;
     S.posted = 0;
+    S.committed = 0;
     S.cap = kp.sv_frames_cap;
     for (uint32_t k = 0; k < HG_SV_RING; ++k) {
         S.uses[k] = 0;
@@ -1075,20 +1078,14 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     return HG_OK;
 }
 
-// Post the next frame to the server, then its gate + blend on the context stream (in frame order, like every other
-// blend).  Frames run at most ring_n ahead of their blends (the host waits for the blend of the frame ring_n back before
-// reusing its ring slot).  The post is the host's half of the close handshake (hg_mega.hip sv_close): raise the post
+// Post frame k = S.posted to the server: the host's half of the close handshake (hg_mega.hip sv_close).  Raise the post
 // word, then read the closing word.  Not raised: the post is taken (a wave that closes later reads the post word after
 // this store).  Raised: the post is taken only if the closing wave's read of the post word included it (the close
-// word); else HG_E_UNSUPPORTED, nothing queued: the caller restarts the server and posts there.
-int server_post(hg_ctx* c) {
+// word); else HG_E_UNSUPPORTED, nothing posted: the caller restarts the server and posts there.  The ring slot must be
+// free (its frame ring_n back blended).
+int server_post_frame(hg_ctx* c) {
     hg_ctx::Server& S = c->sv;
     const uint32_t k = S.posted, s = k & (S.ring_n - 1u);
-    if (S.blend_valid[s]) {
-        sv_trace("post %u: waiting for the blend of frame %u", k, k - S.ring_n);
-        HG_HIP(c, hipEventSynchronize(S.blended[s]));
-        sv_trace("post %u: waited", k);
-    }
     __atomic_store_n(&S.host[HG_SV_HOST_POST], static_cast<unsigned long long>(k + 1u), __ATOMIC_SEQ_CST);
     if (__atomic_load_n(&S.host[HG_SV_HOST_CLOSING], __ATOMIC_SEQ_CST) != 0ull) {
         // the closing wave publishes the post word it read right after reading it (bounded wait: a wave that raised
@@ -1107,6 +1104,27 @@ int server_post(hg_ctx* c) {
         sv_trace("post %u: taken by a closing server", k);
     }
     S.uses[s]++;
+    S.posted = k + 1u;
+#if HG_SV_DIAG_TIMES
+    if (k < 256u) S.post_s[k] = host_seconds();
+#endif
+    return HG_OK;
+}
+
+// The frame the host asks for next (FrameCount = first + committed): posted now, unless it was posted ahead
+// (server_speculate), then its gate + blend on the context stream (in frame order, like every other blend).  Frames run
+// at most ring_n ahead of their blends (the host waits for the blend of the frame ring_n back before reusing its ring
+// slot).  HG_E_UNSUPPORTED: the post was refused (a closing server), nothing queued.
+int server_commit(hg_ctx* c) {
+    hg_ctx::Server& S = c->sv;
+    const uint32_t k = S.committed, s = k & (S.ring_n - 1u);
+    if (k == S.posted) {
+        if (S.blend_valid[s]) {
+            sv_trace("post %u: waiting for the blend of frame %u", k, k - S.ring_n);
+            HG_HIP(c, hipEventSynchronize(S.blended[s]));
+        }
+        if (int rc = server_post_frame(c)) return rc;
+    }
     const uint32_t tiles = uint32_t(c->n_local_tiles), n_slots = tiles * 64u;
     void* err = nullptr;
     HG_HIP(c, hipHostGetDevicePointer(&err, S.host + HG_SV_HOST_LOST, 0));
@@ -1120,13 +1138,31 @@ int server_post(hg_ctx* c) {
                                      c->acc_epoch, c->stream));
     HG_HIP(c, hipEventRecord(S.blended[s], c->stream));
     S.blend_valid[s] = true;
-    S.posted = k + 1u;
-#if HG_SV_DIAG_TIMES
-    if (k < 256u) S.post_s[k] = host_seconds();
-#endif
+    S.committed = k + 1u;
     c->server_frames++;
-    sv_trace("posted %u (slot %u, target %u)", k, s, S.uses[s] * tiles);
+    sv_trace("committed %u (slot %u, target %u)", k, s, S.uses[s] * tiles);
     return HG_OK;
+}
+
+// Frames traced ahead of the host's calls (HG_OPT_SERVER_AHEAD, with the counters off): the next frames of the same
+// parameters and FrameCount chain are posted without a gate or blend, never waiting (a ring slot whose blend has not
+// run stops it).  A call that continues the chain commits them (server_commit); anything else stops the server and
+// abandons those not yet claimed.  The host's display of frame k then waits only for frame k's gate, blend and copy:
+// frame k + 1 is already being traced.  Same images (a frame is blended only when the host asks for it).
+void server_speculate(hg_ctx* c) {
+    hg_ctx::Server& S = c->sv;
+    if (c->sv_ahead <= 0 || c->counters_on) return;
+    const uint32_t ahead = std::min<uint32_t>(uint32_t(c->sv_ahead), S.ring_n - 2u);
+    while (S.posted < S.committed + ahead && S.posted < S.cap) {
+        const uint32_t s = S.posted & (S.ring_n - 1u);
+        if (S.blend_valid[s]) {
+            const hipError_t q = hipEventQuery(S.blended[s]);
+            (void)hipGetLastError();  // hipErrorNotReady is a status here
+            if (q != hipSuccess) return;
+        }
+        if (server_post_frame(c) != HG_OK) return;  // (refused: the next call restarts the server)
+        c->server_ahead_posts++;
+    }
 }
 
 // n_frames frames from FrameCount = params.frameCount through the server (started or restarted as needed).  A first
@@ -1143,7 +1179,7 @@ int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
                 if (rc == HG_E_UNSUPPORTED && f > 0) return fail(c, HG_E_HIP, "render server: restart failed");
                 if (rc) return rc;
             }
-            const int rc = server_post(c);
+            const int rc = server_commit(c);
             if (rc != HG_E_UNSUPPORTED) {
                 if (rc) return rc;
                 break;
@@ -1151,19 +1187,31 @@ int server_render(hg_ctx* c, const HgKernelParams& kp, int32_t n_frames) {
             if (attempt >= 64) return fail(c, HG_E_HIP, "render server: 64 fresh servers in a row refused a post");
         }
     }
+    server_speculate(c);
     return HG_OK;
 }
 
-// The host runs ahead of the GPU: the render call before the previous one has not finished on the device.  Only then
-// does the render server pay: it removes the drain at each frame's end, which a host that waits for every frame (a
-// display at once, or one frame behind) never sees behind its own wait, while the server's resident waves slow the
-// display's untile and copy beside them.
+// The host runs ahead of the GPU: the render call before the previous one has not finished on the device.  Then the
+// render server pays: it removes the drain at each frame's end.  A host that waits for every frame (a display at once,
+// or one frame behind) never runs ahead; the server serves it when it traces ahead of the calls (server_chain).
 bool host_ahead(hg_ctx* c) {
     const int k = int(c->calls & 1u);  // recorded by the call before last
     if (!c->call_done_valid[k]) return false;
     const hipError_t q = hipEventQuery(c->call_done[k]);
     (void)hipGetLastError();  // hipErrorNotReady is a status here
     return q == hipErrorNotReady;
+}
+// The call continues a chain of at least two calls (same parameters, FrameCount continuing) and the server may trace
+// ahead of it (HG_OPT_SERVER_AHEAD, counters off): the frames the host waits for are then already in flight
+bool server_chain(hg_ctx* c, int32_t n_frames) {
+    hg_params q = c->params;
+    q.frameCount = 0;
+    const bool cont = c->chain_len > 0 && c->params.frameCount == c->chain_next &&
+                      std::memcmp(&q, &c->chain_params, sizeof q) == 0;
+    c->chain_len = cont ? c->chain_len + 1 : 1;
+    c->chain_params = q;
+    c->chain_next = c->params.frameCount + n_frames;
+    return c->sv_ahead > 0 && !c->counters_on && c->chain_len >= 2;
 }
 // After a render call's work is queued: its completion event, for host_ahead
 void note_call(hg_ctx* c) {
@@ -1283,6 +1331,12 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             // -> 2,440 vs 2,337, C2 / C5 2 vs 3 -> +1.5 / +2.7 %, C3 at N=1 stays unsplit (tools/sweeps/sweep82-83.txt;
             // the multiplier was 16, then 12 with the chunk-major cost order)
             else split = int(std::min<int64_t>(n_frames, (6 * resident + units - 1) / units));
+            // a share that runs the queue form (HG_OPT_QUEUE_FILL, below): smaller units, about 24 per wave slot, so
+            // the launch's end leaves little behind (emulated N = 8 share of C3: split 8 / 16 / 32 -> 2,708 / 2,861 /
+            // 2,933 Mpaths/s; per-tile waves at split 8: 2,790)
+            if (c->frame_split <= 0 && kern == HG_KERNEL_MEGA_STREAM && n_frames > HG_QUEUE_MAX_FRAMES &&
+                c->queue_fill > 0 && units < int64_t(c->queue_fill) * resident)
+                split = int(std::min<int64_t>(n_frames, (int64_t(HG_QUEUE_FILL_UNITS) * resident + units - 1) / units));
         }
         // the AQL dispatch packet's grid size is a 32-bit count of work-items: at most 2^26 - 1 waves of 64 lanes
         constexpr int64_t kMaxWaves = (int64_t(1) << 26) - 1;
@@ -1316,8 +1370,9 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
 
         c->counters.last_kernel = uint64_t(regen ? kern : HG_KERNEL_MEGA);
         // the reference's one frame per call: posted to the render server (persistent trace waves)
+        const bool chain = accumulate && server_chain(c, n_frames);
         if (c->server_on && stream_k && pipelined && accumulate && n_frames <= HG_QUEUE_MAX_FRAMES && tiles > 0 &&
-            (c->server_on == 2 || host_ahead(c))) {
+            (c->server_on == 2 || host_ahead(c) || chain)) {
             const int rc = server_render(c, kp, n_frames);
             if (rc == HG_OK) {
                 HG_HIP(c, hipEventRecord(ev.second, c->stream));
@@ -1611,8 +1666,39 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
                     c->rb_pending);
     if (int rc = set_device(c)) return rc;
     const int k = c->rb_next;  // not outstanding: at most rb_depth are, and k is the slot after the newest
-    // HG_OPT_READBACK_STREAM: the slot's own device image, copied on the side stream, so the context stream (the next
-    // frames' blends) does not wait for the copy; else c->image, copied on the context stream
+    // HG_OPT_READBACK_STREAM 2 (zero copy): the untile kernel writes the display image straight into the slot's pinned
+    // host image (mapped, fine-grained: its stores cross PCIe as they retire), no copy; the copy event is recorded
+    // after the kernel on the context stream
+    if (c->rb_side == 2) {
+        const size_t bytes = size_t(c->W) * size_t(c->H) * display_bpp(format);
+        if (c->image_host_cap[k] < bytes || !c->image_host_mapped[k]) {
+            if (c->image_host[k]) {
+                HG_HIP(c, hipEventSynchronize(c->image_copied[k]));  // (its last copy was ended: returns at once)
+                HG_HIP(c, hipHostFree(c->image_host[k]));
+            }
+            c->image_host[k] = nullptr;
+            c->image_host_cap[k] = 0;
+            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->image_host[k]), bytes,
+                                         hipHostMallocMapped | hipHostMallocCoherent);
+            if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipHostMalloc(%zu, mapped) failed: %s", bytes, hipGetErrorString(e));
+            c->image_host_cap[k] = bytes;
+            c->image_host_mapped[k] = true;
+            if (!c->image_copied[k]) HG_HIP(c, hipEventCreateWithFlags(&c->image_copied[k], hipEventDisableTiming));
+        }
+        void* dptr = nullptr;
+        HG_HIP(c, hipHostGetDevicePointer(&dptr, c->image_host[k], 0));
+        if (rows) launch_untile<true>(c, dptr, format, static_cast<const float4*>(rows));
+        else launch_untile<false>(c, dptr, format, static_cast<const float4*>(c->acc.p));
+        HG_HIP(c, hipGetLastError());
+        HG_HIP(c, hipEventRecord(c->image_copied[k], c->stream));
+        c->image_host_bytes[k] = bytes;
+        c->image_host_format[k] = format;
+        c->rb_next = (k + 1) % c->rb_depth;
+        c->rb_pending++;
+        return HG_OK;
+    }
+    // HG_OPT_READBACK_STREAM 1: the slot's own device image, copied on the side stream, so the context stream (the next
+    // frames' blends) does not wait for the copy; 0: c->image, copied on the context stream
     const bool side = c->rb_side != 0;
     if (side && !c->rb_stream) {
         // the copy stream on a hardware queue of its own (a plain stream shares one with a trace lane and waits behind
@@ -1631,6 +1717,7 @@ int hg_ctx_display_begin(hg_ctx* c, const void* rows, int32_t format) {
         }
         c->image_host[k] = nullptr;
         c->image_host_cap[k] = 0;
+        c->image_host_mapped[k] = false;
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->image_host[k]), bytes, 0);
         if (e != hipSuccess) return fail(c, HG_E_NOMEM, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
         c->image_host_cap[k] = bytes;
@@ -1849,6 +1936,7 @@ int hg_get_counters(const hg_ctx* cc, hg_counters* out) {
     out->server_frames = c->server_frames;
     server_note_lost(c);
     out->server_refused = c->server_refused;
+    out->server_ahead = c->server_ahead_posts;
     out->frames_lost = c->frames_lost;
     return HG_OK;
 }
@@ -1928,7 +2016,8 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
             return HG_OK;
         case HG_OPT_READBACK_STREAM:
             if (c->rb_pending) return fail(c, HG_E_INVALID, "readbacks outstanding: end them before changing the stream");
-            c->rb_side = value ? 1 : 0;
+            if (value < 0 || value > 2) return fail(c, HG_E_INVALID, "HG_OPT_READBACK_STREAM %d: expected 0, 1 or 2", value);
+            c->rb_side = value;
             return HG_OK;
         case HG_OPT_FRAME_SPLIT:
             if (value < 0 || value > 4096) return fail(c, HG_E_INVALID, "frame split must be 0 (auto)..4096");
@@ -1944,6 +2033,10 @@ int hg_set_option(hg_ctx* c, int32_t option, int32_t value) {
         case HG_OPT_QUEUE_FILL:
             if (value < 0 || value > 64) return fail(c, HG_E_INVALID, "queue fill threshold must be 0 (off)..64 rounds");
             c->queue_fill = value;
+            return HG_OK;
+        case HG_OPT_SERVER_AHEAD:
+            if (value < 0 || value > HG_SV_RING - 2) return fail(c, HG_E_INVALID, "server ahead must be 0..%d", HG_SV_RING - 2);
+            c->sv_ahead = value;
             return HG_OK;
         case HG_OPT_SERVER_IDLE_US:
             if (value < 0 || value > 40000000) return fail(c, HG_E_INVALID, "server idle time must be 0..40000000 us");

@@ -86,7 +86,8 @@ class HgCounters(C.Structure):
                 ("scene_uploads", C.c_uint64), ("scene_uploads_skipped", C.c_uint64),
                 ("scene_uploads_partial", C.c_uint64), ("scene_uploads_vouched", C.c_uint64),
                 ("server_launches", C.c_uint64),
-                ("server_frames", C.c_uint64), ("server_refused", C.c_uint64), ("frames_lost", C.c_uint64)]
+                ("server_frames", C.c_uint64), ("server_refused", C.c_uint64), ("frames_lost", C.c_uint64),
+                ("server_ahead", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if isinstance(v, C.Array) else v)
@@ -108,6 +109,7 @@ HG_OPT_SERVER = 15
 HG_OPT_SERVER_IDLE_US = 16
 HG_OPT_SERVER_GATE_US = 17
 HG_OPT_QUEUE_FILL = 18
+HG_OPT_SERVER_AHEAD = 19
 HG_E_INVALID, HG_E_HIP, HG_E_NOMEM, HG_E_NOSCENE, HG_E_NOTARGET, HG_E_UNSUPPORTED, HG_E_COMM = -1, -2, -3, -4, -5, -6, -7
 HG_E_FRAME_LOST = -8
 HG_READBACK_MAX = 16

@@ -146,6 +146,9 @@ class HalogenRenderPass:
         self.settings = settings
         self.s = clamp_settings(settings)
         self.ctx = context if context is not None else abi.Context(device)
+        # the pass never reads the work counters (the reference has none); off, the render server may trace the next
+        # frames of an unchanged camera ahead of the calls (HG_OPT_SERVER_AHEAD)
+        self.ctx.set_option(abi.HG_OPT_COUNTERS, 0)
         self.FrameCount = 1
         self.AccumulationBufferDirty = True
         self.ObjectBuffersDirty = True

@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
     }
     try {
         halogen::HalogenRenderPass pass(c.settings, argc == 6 ? std::atoi(argv[5]) : 0);
+        pass.SetCounters(true);  // (printed below)
         pass.Execute(scene, c.camera, c.frames);
         const std::vector<float> img = pass.Readback();
         const hg_counters cnt = pass.Counters();

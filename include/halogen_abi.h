@@ -185,6 +185,8 @@ typedef struct hg_counters {
                                        re-posted to a new lifetime; since hg_create */
     uint64_t frames_lost;           /* render server frames whose gate gave up (never 0 on a healthy device: each makes
                                        the accumulation invalid, HG_E_FRAME_LOST), since hg_create */
+    uint64_t server_ahead;          /* frames a render server posted ahead of the host's calls (HG_OPT_SERVER_AHEAD),
+                                       since hg_create */
 } hg_counters;
 
 typedef struct hg_ctx hg_ctx;
@@ -240,8 +242,14 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
        HG_OPT_FRAME_SPLIT = 6, HG_OPT_DESCENT_T = 7, HG_OPT_TILE_ORDER = 8, HG_OPT_COALESCE = 9,
        HG_OPT_READBACK_DEPTH = 10, HG_OPT_READBACK_STREAM = 11, HG_OPT_WAVE_UNITS = 12,
        HG_OPT_LANE_PICK = 14, HG_OPT_SERVER = 15, HG_OPT_SERVER_IDLE_US = 16, HG_OPT_SERVER_GATE_US = 17,
-       HG_OPT_QUEUE_FILL = 18 };
-/* HG_OPT_QUEUE_FILL (default 4): a streaming launch of more than 8 frames whose tiles number fewer than this many rounds
+       HG_OPT_QUEUE_FILL = 18, HG_OPT_SERVER_AHEAD = 19 };
+/* HG_OPT_SERVER_AHEAD (default 4): with the counters off (HG_OPT_COUNTERS 0), the render server traces this many frames
+ *   ahead of the host's calls (the next frames of the same parameters and FrameCount chain), and serves a host that
+ *   waits for every frame (a per-frame display) once two calls continue a chain.  A frame is blended only when the host
+ *   asks for it, so the images are those of one launch per call; frames traced ahead and never asked for (the camera
+ *   moved, the target was read, anything that stops the server) are abandoned, up to a unit per wave of them still
+ *   traced.  0 = never.  (With the counters on, the counters would count frames never asked for: no tracing ahead.) */
+/* HG_OPT_QUEUE_FILL (default 1): a streaming launch of more than 8 frames whose tiles number fewer than this many rounds
  *   of the GPU's wave slots (a rank's 1/N share of the image at N GPUs: strong scaling) runs the persistent work-queue
  *   form, its waves pulling (tile, frame chunk) units instead of one short wave per chunk.  0 = never.  Same images. */
 /* HG_OPT_SERVER (default 1): hg_render calls of at most 8 accumulating frames on the streaming kernel (the reference's
@@ -251,10 +259,11 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
  *   frame's completion, in frame order, so every readback / gather sees exactly the frames rendered before it.  The
  *   server is stopped (its waves trace what was posted, then leave) by uploads, resize, tiling, options, counters,
  *   hg_synchronize, hg_destroy, a launch of another kind, or parameters / FrameCount that do not continue its chain.
- *   1 (automatic) uses the server only while the host runs ahead of the GPU (the call before last still in flight on
- *   the device: a host that queues frames); a host that waits for each frame (a display at once or one frame behind)
- *   launches per call, which measured faster there.  2 = always (while the calls qualify).  0 = every call launches
- *   (the round-4 per-launch pipeline).  Same images either way.
+ *   1 (automatic) uses the server while the host runs ahead of the GPU (the call before last still in flight on the
+ *   device: a host that queues frames), and, when it may trace ahead (HG_OPT_SERVER_AHEAD, counters off), once two
+ *   calls continue a chain (a host that waits for each frame: a per-frame display); otherwise a call launches.
+ *   2 = always (while the calls qualify).  0 = every call launches (the round-4 per-launch pipeline).  Same images
+ *   either way.
  * HG_OPT_SERVER_IDLE_US (default 200000): a server with nothing new posted for this long closes itself (its waves
  *   leave the GPU).  Whether a post is taken never depends on a clock: one wave closes the server by a handshake with
  *   the host's post (both store, then load), and a post the closing wave did not see is re-posted to a new server
@@ -263,7 +272,8 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
  *   frame still short once every wave of its server has left is lost at once.  For tests and diagnostics. */
 /* HG_OPT_READBACK_STREAM: 1 = each display readback is untiled into a device image of its own and copied to the host
  *   on a side stream, so the context stream (the next frames' blends) never waits for a copy; 0 = untiled into one
- *   device image and copied on the context stream.  Same images either way. */
+ *   device image and copied on the context stream; 2 = zero copy: the untile kernel writes the display image straight
+ *   into the ring's pinned host image (mapped, fine-grained), no copy.  Same images either way. */
 #define HG_READBACK_MAX 16
 /* HG_OPT_WAVE_UNITS: streaming launches of more than 8 frames without a frame split, tiles traced per wave (1..4;
  *   0 = automatic, which is 1: more tiles per wave measured slower).  Images whose size is not

@@ -180,7 +180,13 @@ class HalogenRenderPass {
     explicit HalogenRenderPass(const HalogenSettings& settings, int device = 0)
         : settings_(settings), s_(clamp_settings(settings)) {
         check(hg_create(device, &ctx_), "hg_create");
+        // the pass never reads the work counters (the reference has none); off, the render server may trace the next
+        // frames of an unchanged camera ahead of the calls (HG_OPT_SERVER_AHEAD): a per-frame display stops waiting
+        // on each frame's trace
+        check(hg_set_option(ctx_, HG_OPT_COUNTERS, 0), "hg_set_option(HG_OPT_COUNTERS)");
     }
+    // The library's work counters (Counters()) on or off (off by default in the pass)
+    void SetCounters(bool on) { check(hg_set_option(ctx_, HG_OPT_COUNTERS, on ? 1 : 0), "hg_set_option(HG_OPT_COUNTERS)"); }
     HalogenRenderPass(const HalogenRenderPass&) = delete;
     HalogenRenderPass& operator=(const HalogenRenderPass&) = delete;
     ~HalogenRenderPass() { Dispose(); }

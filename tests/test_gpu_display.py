@@ -19,7 +19,7 @@ def _bits(a):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("side", [0, 1])
+@pytest.mark.parametrize("side", [0, 1, 2])
 @pytest.mark.parametrize("fmt", FORMATS)
 def test_gpu_display_format_equals_host_packing(gpu, fmt, side):
     packed, params, cube, frames, acc = cases.setup("glass_64x36")  # emissive + sky: values above 1 and tiny ones
@@ -31,7 +31,7 @@ def test_gpu_display_format_equals_host_packing(gpu, fmt, side):
             ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
         ctx.resize(W, H)
         ctx.set_params(params)
-        ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)  # copies on the context stream or on the side stream
+        ctx.set_option(abi.HG_OPT_READBACK_STREAM, side)  # copies on the context or side stream, or zero copy
         ctx.render(1, True)
         ctx.readback_begin(fmt)
         got = [ctx.readback_end(W, H)]  # frame 1, at once

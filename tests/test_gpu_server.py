@@ -145,12 +145,25 @@ def test_gpu_server_restarts_keep_the_image(gpu):
     checkpoint (set_accumulation), a clear alone (the server keeps running: the clear is ordered between blends), a
     counters read, a launch of another kind (a 16-frame call), short idle gaps (the server stays), an idle gap longer
     than the server's idle time (it closes itself; the next post restarts it), an upload."""
+    on, con = _restart_sequence(2)
+    off, coff = _restart_sequence(0)
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert_bitwise(a, b, f"server restarts, readback {k}")
+    assert con["server_launches"] >= 6 and coff["server_launches"] == 0, (con, coff)
+    for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
+        assert con[k] == coff[k], (k, con[k], coff[k])
+
+
+def _restart_sequence(server, options=()):
+    """The call sequence of test_gpu_server_restarts_keep_the_image: its readbacks and the counters."""
     packed, params, cube, _, _ = cases.setup("dragon10_64x36")
     moved = cases.setup("dragon10_64x36")[1]
     moved.camLocalToWorld.m[12] += 0.05
 
     def run(server):
         ctx, W, H = _ctx(packed, params, cube, server=server)
+        for opt, v in options:
+            ctx.set_option(opt, v)
         imgs = []
         with ctx:
             def frames(k):
@@ -181,13 +194,7 @@ def test_gpu_server_restarts_keep_the_image(gpu):
             cnt = ctx.counters()
         return imgs, cnt
 
-    on, con = run(2)
-    off, coff = run(0)
-    for k, (a, b) in enumerate(zip(on, off)):
-        assert_bitwise(a, b, f"server restarts, readback {k}")
-    assert con["server_launches"] >= 6 and coff["server_launches"] == 0, (con, coff)
-    for k in ("paths", "rays", "tri_tests", "aabb_tests", "hits"):
-        assert con[k] == coff[k], (k, con[k], coff[k])
+    return run(server)
 
 
 @pytest.mark.gpu
@@ -338,3 +345,43 @@ def test_gpu_server_lost_frame_leaves_the_accumulator(gpu, tiling):
         again = np.full((H, W, 4), np.nan, np.float32)
         ctx.readback(W, H, again)
     assert_bitwise(again, want3, "3 frames after the clear")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ahead", [1, 2, 4])
+def test_gpu_server_traces_ahead_keeps_the_image(gpu, ahead):
+    """HG_OPT_SERVER_AHEAD with the counters off: the server traces `ahead` frames beyond the host's calls and blends
+    a frame only when it is asked for.  The restart sequence (camera moves, checkpoint, clears, counters, a 16-frame
+    launch, idle gaps, an upload: each abandons the frames traced ahead) gives the readbacks of the server off, bit for
+    bit; so does a per-frame display at once and one frame behind, in the automatic mode (HG_OPT_SERVER 1), where the
+    call chain engages the server although the host never runs ahead."""
+    opts = ((abi.HG_OPT_COUNTERS, 0), (abi.HG_OPT_SERVER_AHEAD, ahead))
+    on, con = _restart_sequence(2, opts)
+    off, _ = _restart_sequence(0, opts)
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert_bitwise(a, b, f"ahead {ahead}: server restarts, readback {k}")
+    assert con["server_ahead"] > 0 and con["frames_lost"] == 0, con
+    packed, params, cube, _, _ = cases.setup("dragon10_64x36")
+    n = 12
+    want = [gpu_render(packed, params, k, True, cube)[0] for k in range(1, n + 1)]
+    for depth in (1, 2):
+        ctx, W, H = _ctx(packed, params, cube, server=1)
+        with ctx:
+            for opt, v in opts:
+                ctx.set_option(opt, v)
+            ctx.set_option(abi.HG_OPT_READBACK_DEPTH, depth)
+            got, pending = [], 0
+            for _ in range(n):
+                ctx.render(1, True)
+                ctx.readback_begin(abi.HG_DISPLAY_RGBA32F)
+                pending += 1
+                if pending == depth:
+                    got.append(ctx.readback_end(W, H))
+                    pending -= 1
+            while pending:
+                got.append(ctx.readback_end(W, H))
+                pending -= 1
+            cnt = ctx.counters()
+        for k, img in enumerate(got):
+            assert_bitwise(img, want[k], f"ahead {ahead}, display depth {depth}, frame {k + 1}")
+        assert cnt["server_launches"] >= 1 and cnt["server_frames"] >= n - 1 and cnt["server_ahead"] > 0, cnt
