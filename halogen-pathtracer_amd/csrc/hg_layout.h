@@ -75,9 +75,6 @@
 // waves issue first) and 0 while shading (C3 2,097 -> 2,111, tools/sweeps/sweep67-68.txt); the regenerating kernel's
 // at 1 during get_ray_intersection (C2 +1 %, C5 +2 %, tools/sweeps/sweep69.txt).
 #define HG_TRAVERSE_PRIO 1
-#ifndef HG_DRAIN_PRIO
-#define HG_DRAIN_PRIO 0  // queue launches: waves whose queue ran dry issue at priority 3 / 2 (traversal / shading)
-#endif
 #ifndef HG_TILE_ORDER
 #define HG_TILE_ORDER 1  // regen / stream kernels: dispatch tiles in descending cost of the previous launch (hg_order_tiles)
 #endif

@@ -1365,10 +1365,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 cyc_trav += t;
                 cyc_shade -= t;
             }
-            // (HG_DRAIN_PRIO, queue launches: a wave whose queue ran dry holds the launch's last paths; it issues ahead of
-            // the next launch's waves, so the frame completes sooner: the latency a per-frame display waits on)
-            if (HG_DRAIN_PRIO && kQueue && !kServer && dry) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
             // ---- finished lanes: shade, then start their next ray (a ray with nothing to traverse shades again)
             // (rays that finish at once — everything culled — shade again in this loop while at least
             // HG_STREAM_RESHADE lanes need it, otherwise in the next shading phase)
@@ -1477,8 +1474,7 @@ __global__ __launch_bounds__(HG_STREAM_LB, HG_STREAM_WAVES) void hg_trace_stream
                 if (alive) trav_begin<kMeshLds>(kp, ray, tv, c);
                 }
             }
-            if (HG_DRAIN_PRIO && kQueue && !kServer && dry) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
+            __builtin_amdgcn_s_setprio(HG_TRAVERSE_PRIO);
             if (kCounters) cyc_shade += wave_clock();
         }
         if constexpr (!kServer) {
