@@ -133,9 +133,9 @@
 #define HG_WAVE_UNITS_LIMIT 4  // HG_OPT_WAVE_UNITS range (the units' tiles sit in scalar registers)
 #ifndef HG_QUEUE_FILL
 // default HG_OPT_QUEUE_FILL: streaming launches of more than HG_QUEUE_MAX_FRAMES frames whose tiles give fewer rounds of
-// the GPU's wave slots than this run the queue form (a rank's share at N = 8, 1080p: 0.79 rounds).  The queue form
-// costs 13 % per item against per-tile waves (C3 at N = 1: 3,042 vs 3,491 Mpaths/s; same instruction counts), so it
-// pays only below one round (emulated N = 4 share, 1.58 rounds: 2,842 vs 3,114)
+// the GPU's wave slots than this run the queue form (a rank's share at N = 8, 1080p: 0.79 rounds).  With about 24
+// (tile, frame chunk) units per wave slot the queue form costs 6 % against per-tile waves at N = 1 (C3: 3,288 vs 3,491
+// Mpaths/s); emulated shares, queue vs per-tile: N = 2 3,229 vs 3,366, N = 4 3,114 vs 3,122, N = 8 2,937 vs 2,803
 #define HG_QUEUE_FILL 1
 #endif
 #define HG_QUEUE_FILL_UNITS 24  // queue-form shares: (tile, frame chunk) units per wave slot

@@ -10,7 +10,6 @@ for n in ${RANKS:-2 4 8}; do
         --no-fast-bvh --steps ${STEPS:-8} ${EXTRA:-} > $O/n${n}_f${f}.json 2> $O/n${n}_f${f}.err || { tail -5 $O/n${n}_f${f}.err; exit 1; }
     python3 -c "
 import json; r = json.loads(open('$O/n${n}_f${f}.json').read().strip().splitlines()[-1]); s = r['strong_scaling']
-print('N=$n fill=$f weak %.0f strong %.0f (per-GPU frac of weak %.3f) ms/step %.3f' % (r['value'], s['value'],
-      s.get('per_gpu_frac_of_weak', 0), s['ms_per_step']))"
+print('N=$n fill=$f weak %.0f strong %.0f ms/step %.3f' % (r['value'], s['value'], s['ms_per_step']))"
   done
 done
