@@ -976,8 +976,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     const size_t per_frame = size_t(tiles) * 64u * sizeof(float4);
     uint32_t ring = HG_SV_RING;
     while (ring > 2u && size_t(ring) * per_frame > (size_t(2) << 30)) ring >>= 1;
-    // waves per SIMD: HG_SV_WAVES (HALOGEN_SERVER_WAVES overrides, 1..HG_STREAM_WAVES, for A/B; fewer leave wave slots
-    // to the kernels the context stream runs between the server's frames, and measured slower)
+    // waves per SIMD: HG_SV_WAVES, the kernel's occupancy (HALOGEN_SERVER_WAVES overrides, 1..HG_STREAM_WAVES, for A/B)
     static const uint32_t sv_waves = [] {
         const char* e = std::getenv("HALOGEN_SERVER_WAVES");
         const int v = e ? std::atoi(e) : 0;
