@@ -60,3 +60,26 @@ def test_a_failing_rank_fails_the_parent():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-probe"], cwd=ROOT,
                        env=_env(HALOGEN_BENCH_PROBE_FAIL_RANK="1"), capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
+
+
+def test_compact_summary_and_detail_split(tmp_path):
+    """The line's last key (`summary`) carries the per-frame operating points; the per-format display tables go to the
+    detail file and the line keeps the reference's display format."""
+    import bench
+    disp = {f: {"sync": {"frac_of_batched": 0.7}, "pipelined": {"frac_of_batched": 0.8}} for f in ("rgba32f", "rgba16f",
+                                                                                                 "r11g11b10f")}
+    result = {"value": 3500.0, "primary_miss_frac": 0.54, "roofline": {"frac": 0.56}, "config": {"workload": "C3"},
+              "per_frame": {"frac_of_batched": 0.96, "strict": {"value": 3150.0, "frac_of_batched": 0.9,
+                                                                  "per_launch": {"frac_of_batched": 0.85}},
+                            "with_display_readback": disp},
+              "camera_move": {"value": 1860.0, "upload_share": 0.003}, "framed": {"value": 1650.0}}
+    out = tmp_path / "detail.json"
+    bench.split_detail(result, str(out))
+    assert set(result["per_frame"]["with_display_readback"]) == {"r11g11b10f", "other_formats"}
+    assert json.loads(out.read_text())["with_display_readback"]["rgba16f"]["sync"]["frac_of_batched"] == 0.7
+    s = bench.compact_summary(result)
+    assert s["per_frame"]["strict"]["frac_of_batched"] == 0.9
+    assert s["per_frame"]["display_r11g11b10f"]["at_once"] == 0.7
+    assert s["per_frame"]["display_r11g11b10f"]["one_behind"] == 0.8
+    assert s["camera_move"]["frac_of_batched"] == round(1860 / 3500, 3) and s["framed"] == 1650.0
+    assert len(json.dumps(s)) < 1000

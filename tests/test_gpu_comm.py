@@ -186,3 +186,55 @@ def test_gpu_comm_display_readback_pipelined(gpu, transport):
         comm.close()
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_comm_gather_refuses_a_lost_frame(gpu):
+    """A rank whose accumulation a lost render-server frame invalidated (HG_OPT_SERVER_GATE_US 0 on a 1080p C3 frame:
+    its gate finds it unfinished) makes the gather fail with HG_E_FRAME_LOST (the peer transport checks every member;
+    the RCCL one carries the flag in its agreement all-reduce); after a clear of that rank the gather works again and
+    the image equals one context's."""
+    from halogen import scenes
+    from test_gpu_server import _sized
+    cfg = scenes.CONFIGS["C3"]
+    packed, params, cube = _sized("C3", cfg.width, cfg.height)
+    W, H = cfg.width, cfg.height
+    ctxs = []
+    for r in range(2):
+        ctx = abi.Context(0)
+        ctx.set_option(abi.HG_OPT_SERVER, 2)
+        ctx.set_option(abi.HG_OPT_COALESCE, 1)
+        ctx.upload_scene(packed)
+        if cube is not None:
+            ctx.upload_cubemap(cube.face_size, cube.n_mips, cube.texels)
+        ctx.resize(W, H)
+        ctx.set_tiling(r, 2)
+        ctx.set_params(params)
+        ctxs.append(ctx)
+    comm = abi.Comm.all(ctxs)
+    try:
+        ctxs[0].render(1, True)
+        ctxs[1].set_option(abi.HG_OPT_SERVER_GATE_US, 0)
+        try:
+            ctxs[1].render(1, True)
+        except abi.HalogenError as e:
+            assert e.rc == abi.HG_E_FRAME_LOST, e
+        with pytest.raises(abi.HalogenError) as e:
+            ctxs[1].synchronize()  # (the frame's gate has given up by the time the server is stopped)
+        assert e.value.rc == abi.HG_E_FRAME_LOST
+        with pytest.raises(abi.HalogenError) as e:
+            comm.gather(0)
+        assert e.value.rc == abi.HG_E_FRAME_LOST, e.value
+        ctxs[1].set_option(abi.HG_OPT_SERVER_GATE_US, -1)
+        ctxs[1].clear_accumulation()
+        ctxs[1].set_params(params)
+        ctxs[1].render(1, True)
+        comm.gather(0)
+        img = comm.readback(W, H)
+        with abi.Context(0) as one:
+            ref, _ = gpu_render(packed, params, 1, True, cube, ctx=one)
+        assert_bitwise(img, ref, "gathered image after the lost rank's clear")
+    finally:
+        comm.close()
+        for c in ctxs:
+            c.close()
