@@ -293,7 +293,8 @@ def test_gpu_server_posts_racing_the_close_handshake(gpu, idle_us):
         assert_bitwise(img, ref, f"idle {idle_us} us, {per_call} per call: {cnt['server_launches']} lifetimes, "
                                  f"{cnt['server_refused']} posts refused")
         assert cnt["server_frames"] == frames and cnt["frames_lost"] == 0 and cnt["paths"] == rc["paths"], cnt
-        assert cnt["server_launches"] > 1, cnt  # the server closed between posts at least once
+        if idle_us == 0:  # (at 30 us the host's posts may all come sooner than that: no close is guaranteed)
+            assert cnt["server_launches"] > 1, cnt  # the server closed between posts at least once
         print(f"idle {idle_us} us, {per_call} per call: {cnt['server_launches']} lifetimes, "
               f"{cnt['server_refused']} refused posts")
 
