@@ -441,7 +441,7 @@ def camera_move_measurement(ctx, packed, s, cfg, W, H, frames: int, cube) -> dic
 
 
 def strong_scaling_measurement(ctx, params, W, H, fps: int, steps: int, world: int, rank: int, emu: int, barrier,
-                               gather_fn, coll_dev, dist, ref_img=None) -> dict:
+                               gather_fn, coll_dev, dist, ref_img=None, coalesce: int = -1) -> dict:
     """The strong-scaling leg, beside the weak line: the FIXED image of `fps` frames per step (C3: 64),
     its 8x8 tiles dealt round-robin to the N ranks (HC:1033: pixels are independent), so the ranks share one image's work
     instead of each doing one image's worth.  Same clock as the headline (barrier + device sync on both sides, max over
@@ -450,9 +450,12 @@ def strong_scaling_measurement(ctx, params, W, H, fps: int, steps: int, world: i
     shows.  N > 1: rank 0 compares the gathered image with `ref_img` (the same frames on one context, all tiles) bit for
     bit.  --emulate-ranks N (one GPU): rank 0's share alone, and the rate N such shares would reach if equally fast."""
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)
+    if coalesce >= 1:
+        ctx.set_option(abi.HG_OPT_COALESCE, coalesce)
     ctx.clear_accumulation()
     ctx.set_params(params)
-    ctx.render(fps, True)  # warm-up (this share's cost order)
+    for _ in range(steps):  # warm-up: the same calls (this share's launches, their buffers and cost order)
+        ctx.render(fps, True)
     ctx.clear_accumulation()
     ctx.set_params(params)
     ctx.reset_counters()
@@ -747,6 +750,8 @@ def main():
     ap.add_argument("--server-ahead", type=int, default=-1, help="HG_OPT_SERVER_AHEAD (frames traced ahead); -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--no-strong", action="store_true", help="N > 1 / --emulate-ranks: skip the strong-scaling leg")
+    ap.add_argument("--strong-coalesce", type=int, default=-1,
+                    help="the strong leg's HG_OPT_COALESCE (frames held for one launch); -1: the library's default")
     ap.add_argument("--dist-probe", action="store_true",
                     help="launcher check, no GPU: every rank joins the process group, all-reduces its rank, rank 0 prints "
                          "one JSON line (tests/test_bench_launch.py)")
@@ -1104,7 +1109,7 @@ def main():
                     one.render(args.frames_per_step, True)
                 ref_img = one.readback(W, H)
         strong = strong_scaling_measurement(ctx, params, W, H, args.frames_per_step, args.steps, world, rank, emu,
-                                            barrier, strong_gather, coll_dev, dist, ref_img)
+                                            barrier, strong_gather, coll_dev, dist, ref_img, args.strong_coalesce)
 
     total_paths = W * H * frames_per_step * args.steps
     if emu:  # this GPU traced only its 1/N share of the tiles

@@ -139,6 +139,14 @@
 #define HG_QUEUE_FILL 1
 #endif
 #define HG_QUEUE_FILL_UNITS 24  // queue-form shares: (tile, frame chunk) units per wave slot
+#ifndef HG_SHARE_HOLD_ROUNDS
+// A rank's share of the image (hg_set_tiling, N > 1) holds consecutive hg_render calls (HG_OPT_COALESCE > 1) until the
+// held launch has this many rounds of the GPU's wave slots in 64-frame tile waves, as one context's 64-frame launch of
+// the whole 1080p image has (32,400 tiles / 5,120 slots): 8 calls of 64 frames at N = 8, 4 at N = 4, 2 at N = 2.
+// Emulated strong shares of C3 (tools/gpu_strong_coalesce.sh): N = 8 3,000 -> 3,526 Mpaths/s, N = 4 3,128 -> 3,465.
+#define HG_SHARE_HOLD_ROUNDS 6
+#endif
+#define HG_SHARE_HOLD_MAX 1024  // frames: the most a share holds (its frame colours: 2 trace streams x 4 GiB at most)
 #ifndef HG_QUEUE_MAX_FRAMES
 #define HG_QUEUE_MAX_FRAMES 8  // streaming launches of at most this many frames run the persistent work-queue form (kQueue)
 #endif

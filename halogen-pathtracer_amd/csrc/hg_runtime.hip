@@ -1334,7 +1334,7 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
             // the launch's end leaves little behind (emulated N = 8 share of C3: split 8 / 16 / 32 -> 2,708 / 2,861 /
             // 2,933 Mpaths/s; per-tile waves at split 8: 2,790)
             if (c->frame_split <= 0 && kern == HG_KERNEL_MEGA_STREAM && n_frames > HG_QUEUE_MAX_FRAMES &&
-                c->queue_fill > 0 && units < int64_t(c->queue_fill) * resident)
+                c->queue_fill > 0 && units * n_frames < int64_t(c->queue_fill) * resident * 64)
                 split = int(std::min<int64_t>(n_frames, (int64_t(HG_QUEUE_FILL_UNITS) * resident + units - 1) / units));
         }
         // the AQL dispatch packet's grid size is a 32-bit count of work-items: at most 2^26 - 1 waves of 64 lanes
@@ -1459,10 +1459,12 @@ int render_now(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
                 kc.frame_color = static_cast<float4*>(L.frame_color.p);
                 kc.spill = spill_bytes ? static_cast<uint32_t*>(L.spill.p) : nullptr;
                 // the persistent work-queue form for launches of few frames (the reference's one dispatch per frame),
-                // and for a share of the tiles too small to fill the GPU with per-tile waves (a rank's 1/N of the image
-                // at N GPUs, HG_OPT_QUEUE_FILL): persistent waves pull (tile, frame chunk) units, so a wave's lanes
-                // drain once per launch, not once per short wave
-                const bool fill = c->queue_fill > 0 && tiles < int64_t(c->queue_fill) * int64_t(slots);
+                // and for a launch too small to fill the GPU with 64-frame tile waves (a rank's 1/N of the image at N
+                // GPUs, HG_OPT_QUEUE_FILL): persistent waves pull (tile, frame chunk) units, so a wave's lanes drain
+                // once per launch, not once per short wave.  A share's launch of many frames fills the GPU with split
+                // tile waves instead (emulated N = 8 share of C3, 512 frames: queue 3,289, split tile waves 3,543)
+                const bool fill = c->queue_fill > 0 &&
+                                  tiles * int64_t(kc.n_frames) < int64_t(c->queue_fill) * int64_t(slots) * 64;
                 kc.queue = stream_k && (kc.n_frames <= HG_QUEUE_MAX_FRAMES || fill) ? static_cast<uint32_t*>(L.queue.p)
                                                                                      : nullptr;
                 // Persistent waves of a queue launch.  A launch's end costs each of its waves the time its last paths
@@ -1796,6 +1798,21 @@ int hg_pack_display(const float* rgba, size_t n_pixels, int32_t format, void* ou
     return HG_OK;
 }
 
+namespace {
+// Frames of consecutive calls held for one launch (HG_OPT_COALESCE).  A rank's share of the image (N > 1) holds until
+// its launch fills the GPU as one context's launch of the whole image does (HG_SHARE_HOLD_ROUNDS): a 1/8 share's
+// 64-frame launch has 4,050 tiles for 5,120 wave slots, and its tail is as long as a full launch's.
+int32_t hold_window(const hg_ctx* c) {
+    int64_t w = c->coalesce;
+    if (w > 1 && c->n_ranks > 1 && c->n_local_tiles > 0) {
+        const int64_t slots = int64_t(c->n_cu) * 4 * HG_STREAM_WAVES;
+        const int64_t share = (int64_t(HG_SHARE_HOLD_ROUNDS) * slots * 64 + c->n_local_tiles - 1) / c->n_local_tiles;
+        w = std::max(w, std::min<int64_t>(share, HG_SHARE_HOLD_MAX));
+    }
+    return int32_t(w);
+}
+}  // namespace
+
 int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     if (!c) return HG_E_INVALID;
     if (int rc = render_check(c, n_frames)) return rc;
@@ -1809,7 +1826,7 @@ int hg_render(hg_ctx* c, int32_t n_frames, int32_t accumulate) {
     // entry point flushes first)
     c->pending_acc = accumulate;
     c->pending_frames += n_frames;
-    return c->pending_frames >= c->coalesce ? hg_ctx_flush(c) : HG_OK;
+    return c->pending_frames >= hold_window(c) ? hg_ctx_flush(c) : HG_OK;
 }
 
 int hg_synchronize(hg_ctx* c) {

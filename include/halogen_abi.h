@@ -234,7 +234,9 @@ enum { HG_KERNEL_MEGA = 0, HG_KERNEL_WAVEFRONT = 1, HG_KERNEL_MEGA_REGEN = 2, HG
  *   launched together once this many frames are pending (default 32), or as soon as any other entry point is called
  *   (each launches the held frames first).  The frames, their order and the image are those of separate launches; a
  *   launch has a fixed cost (its drain tail: ~0.35 ms on C3), so the reference's one call per frame (RP:327) runs at
- *   the multi-frame rate.  1 = every call launches at once. */
+ *   the multi-frame rate.  A rank's share of the image (hg_set_tiling, N > 1) holds at least until its launch fills the
+ *   GPU as one context's launch of the whole image does (6 rounds of the wave slots in 64-frame tile waves, at most
+ *   1024 frames: 8 calls of 64 frames for a 1/8 share of 1080p).  1 = every call launches at once. */
 /* HG_OPT_READBACK_DEPTH: display readbacks (hg_readback_begin[_format]) that may be outstanding at once, 1..16
  *   (default 2: display one frame behind).  A deeper ring lets a caller that displays every frame keep more frames in
  *   flight (display latency traded for throughput); changing it needs no readback outstanding. */
@@ -249,9 +251,10 @@ enum { HG_OPT_KERNEL = 1, HG_OPT_BLOCK = 2, HG_OPT_COUNTERS = 3, HG_OPT_TIMING =
  *   asks for it, so the images are those of one launch per call; frames traced ahead and never asked for (the camera
  *   moved, the target was read, anything that stops the server) are abandoned, up to a unit per wave of them still
  *   traced.  0 = never.  (With the counters on, the counters would count frames never asked for: no tracing ahead.) */
-/* HG_OPT_QUEUE_FILL (default 1): a streaming launch of more than 8 frames whose tiles number fewer than this many rounds
- *   of the GPU's wave slots (a rank's 1/N share of the image at N GPUs: strong scaling) runs the persistent work-queue
- *   form, its waves pulling (tile, frame chunk) units instead of one short wave per chunk.  0 = never.  Same images. */
+/* HG_OPT_QUEUE_FILL (default 1): a streaming launch of more than 8 frames with fewer than this many rounds of the GPU's
+ *   wave slots in 64-frame tile waves (tiles x frames / 64; a rank's 1/N share of the image at N GPUs launched a call at
+ *   a time) runs the persistent work-queue form, its waves pulling (tile, frame chunk) units instead of one short wave
+ *   per chunk.  0 = never.  Same images. */
 /* HG_OPT_SERVER (default 1): hg_render calls of at most 8 accumulating frames on the streaming kernel (the reference's
  *   one dispatch per frame, RP:327) post their frames to a render server — persistent trace waves that outlive the call
  *   and take each posted frame's (tile, frame) units as soon as lanes free up, so one frame's last paths overlap the

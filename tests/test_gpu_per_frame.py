@@ -106,6 +106,22 @@ def test_gpu_one_frame_launches_match_batched_full_size(gpu, cfg_name):
 
 
 @pytest.mark.gpu
+def test_gpu_share_holds_calls_until_it_fills_the_gpu(gpu):
+    """A rank's 1/8 share of C3 (4,050 of 32,400 tiles) holds consecutive 64-frame calls until its launch has as many
+    rounds of 64-frame tile waves as one context's whole image (HG_SHARE_HOLD_ROUNDS: 8 calls here), and runs one
+    launch of split tile waves; every call its own launch (coalesce 1: the queue form) and one hg_render(512) give the
+    same image, bit for bit."""
+    packed, params, cube = _full("C3")
+    held, hc = gpu_render(packed, params, 512, True, cube, tiling=(0, 8), splits=[64] * 8)
+    strict, sc = gpu_render(packed, params, 512, True, cube, tiling=(0, 8), splits=[64] * 8, coalesce=1)
+    one, _ = gpu_render(packed, params, 512, True, cube, tiling=(0, 8))
+    assert hc["launches"] == 1 and sc["launches"] == 8, (hc["launches"], sc["launches"])
+    assert_bitwise(held, strict, "1/8 share: 8 x render(64) held vs each launched")
+    assert_bitwise(one, strict, "1/8 share: render(512) vs 8 x render(64)")
+    assert hc["paths"] == sc["paths"]
+
+
+@pytest.mark.gpu
 def test_gpu_mixed_launch_sizes_with_tile_order(gpu):
     """1-frame launches between multi-frame ones, with the cost order re-sorted only every 16 frames and a rank's share
     of the tiles: the same image as one launch."""
