@@ -748,6 +748,7 @@ def main():
     ap.add_argument("--no-fast-bvh", action="store_true", help="skip the fast_bvh leg (C3 on an SAH BLAS)")
     ap.add_argument("--queue-fill", type=int, default=-1, help="HG_OPT_QUEUE_FILL (0 off, k rounds); -1: default")
     ap.add_argument("--server-ahead", type=int, default=-1, help="HG_OPT_SERVER_AHEAD (frames traced ahead); -1: default")
+    ap.add_argument("--server-idle-us", type=int, default=-1, help="HG_OPT_SERVER_IDLE_US; -1: default")
     ap.add_argument("--descent-t", type=int, default=-2, help="HG_OPT_DESCENT_T (-1 auto, 0..64); -2: default")
     ap.add_argument("--no-strong", action="store_true", help="N > 1 / --emulate-ranks: skip the strong-scaling leg")
     ap.add_argument("--strong-coalesce", type=int, default=-1,
@@ -843,6 +844,8 @@ def main():
         ctx.set_option(abi.HG_OPT_QUEUE_FILL, args.queue_fill)
     if args.server_ahead >= 0:
         ctx.set_option(abi.HG_OPT_SERVER_AHEAD, args.server_ahead)
+    if args.server_idle_us >= 0:
+        ctx.set_option(abi.HG_OPT_SERVER_IDLE_US, args.server_idle_us)
     ctx.set_option(abi.HG_OPT_COUNTERS, 0)  # timed region: production kernel (counts come from the replay below)
     ctx.upload_scene(packed)
     if cube is not None:

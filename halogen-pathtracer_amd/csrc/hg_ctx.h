@@ -93,6 +93,10 @@ struct hg_ctx {
         uint32_t committed = 0;  // frames the host asked for (gate + blend queued); posted - committed were posted ahead
         uint32_t uses[HG_SV_RING] = {};     // frames posted to each ring slot in this lifetime
         hipEvent_t blended[HG_SV_RING] = {};  // after the blend of each ring slot's last frame
+        // HALOGEN_SERVER_SERIAL=1 (a profiling aid, tools/pmc_server.sh): the gates wait for the lifetime's end (this
+        // event, after the server kernel), so a profiler that runs one kernel at a time (rocprofv3 --pmc) never runs a
+        // gate before the server it waits for
+        hipEvent_t exited = nullptr;
         bool blend_valid[HG_SV_RING] = {};
         hg_params params{};   // the parameters it was started with (frameCount: its first frame)
         int32_t kernel_variant = 0, descent_t = 0;

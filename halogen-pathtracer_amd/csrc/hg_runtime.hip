@@ -551,6 +551,7 @@ void hg_destroy(hg_ctx* c) {
     auto server_events = [&S] {
         for (hipEvent_t& e : S.blended)
             if (e) (void)hipEventDestroy(e);
+        if (S.exited) (void)hipEventDestroy(S.exited);
         sv_trace("destroy: server events destroyed");
     };
     auto server_host = [&S] {
@@ -954,6 +955,16 @@ bool server_continues(hg_ctx* c, int32_t fc) {
 
 // Launch the server for the frames from FrameCount `fc`: kp is the launch's parameter block as render_now built it.  HG_E_UNSUPPORTED when the device gives no stream with a hardware queue of its own (the server's
 // gates on the context stream must never queue behind it): the caller launches per call instead.
+// HALOGEN_SERVER_SERIAL=1: every gate waits for its server lifetime's end (a profiling aid for profilers that run one
+// kernel at a time; the frames are then blended only after the lifetime closes, on idle or at a stop)
+bool server_serial() {
+    static const bool on = [] {
+        const char* e = std::getenv("HALOGEN_SERVER_SERIAL");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
+
 int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     hg_ctx::Server& S = c->sv;
     if (!S.stream) {
@@ -966,6 +977,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
             return HG_E_UNSUPPORTED;
         }
         for (hipEvent_t& e : S.blended) HG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HG_HIP(c, hipEventCreateWithFlags(&S.exited, hipEventDisableTiming));
         // coherent (fine-grained) pinned memory: the pollers' system-scope loads of the post word read host memory
         // itself (measured the same as the default pinned memory, tools/sweeps/sweep_r05_server.txt; this is the
         // memory type whose coherence the loads rely on)
@@ -1058,6 +1070,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     __atomic_store_n(&S.host[HG_SV_HOST_CLOSING], 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(&S.host[HG_SV_HOST_CLOSED], 0ull, __ATOMIC_SEQ_CST);
     HG_HIP(c, hg_launch_mega_stream(kp, 64, c->counters_on != 0, S.stream, true));
+    if (server_serial()) HG_HIP(c, hipEventRecord(S.exited, S.stream));
     S.running = true;
     S.ring_n = ring;
     S.posted = 0;
@@ -1127,6 +1140,7 @@ int server_commit(hg_ctx* c) {
     const uint32_t tiles = uint32_t(c->n_local_tiles), n_slots = tiles * 64u;
     void* err = nullptr;
     HG_HIP(c, hipHostGetDevicePointer(&err, S.host + HG_SV_HOST_LOST, 0));
+    if (server_serial()) HG_HIP(c, hipStreamWaitEvent(c->stream, S.exited, 0));
     HG_HIP(c, hg_launch_server_frame(static_cast<float4*>(c->acc.p),
                                      static_cast<const float4*>(S.ring.p) + size_t(s) * n_slots, n_slots,
                                      S.kp.first_frame + int32_t(k), static_cast<const uint32_t*>(S.done.p) + 32u * s,
