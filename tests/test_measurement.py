@@ -70,12 +70,12 @@ def test_roofline_prices_the_binding_unit(bench, monkeypatch):
 
 
 def test_committed_bench_line_keeps_the_contract():
-    """The round's committed bench line (profiles/r06_bench.json, the shipped library on the GPU box) carries the
+    """The round's committed bench line (profiles/r06f_bench.json, the shipped library on the GPU box) carries the
     driver's contract keys, the roofline priced on the vector-memory unit from the committed profile of the same
     library, the cpu_baseline, and the second numbers beside the headline (framed, per_frame, fast_bvh)."""
     import json
 
-    line = json.loads((ROOT / "profiles" / "r06_bench.json").read_text().strip().splitlines()[-1])
+    line = json.loads((ROOT / "profiles" / "r06f_bench.json").read_text().strip().splitlines()[-1])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in line, k
@@ -83,7 +83,7 @@ def test_committed_bench_line_keeps_the_contract():
     assert line["config"]["workload"].startswith("C3") and line["config"]["frames_per_step"] == 64
     r = line["roofline"]
     assert r["bound"] == "vmem" and r["counters_library_matches"] is True
-    assert r["counters_from"] == "profiles/r06_C3_summary.json" and (ROOT / r["counters_from"]).exists()
+    assert r["counters_from"] == "profiles/r06f_C3_summary.json" and (ROOT / r["counters_from"]).exists()
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and 0.3 < r["frac"] < 1.0
     cpu = line["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
@@ -92,7 +92,7 @@ def test_committed_bench_line_keeps_the_contract():
     assert {"coalesce_1", "coalesce_32"} <= set(ident) and all(ident.values()), ident
     # the operating points as the line's last key, inside the driver's 8-KB tail
     assert list(line)[-1] == "summary"
-    tail = (ROOT / "profiles" / "r06_bench.json").read_text()[-8192:]
+    tail = (ROOT / "profiles" / "r06f_bench.json").read_text()[-8192:]
     assert '"strict": {"value"' in tail and '"one_behind"' in tail
     sm = line["summary"]
     assert sm["per_frame"]["strict"]["frac_of_batched"] > 0.85
@@ -101,4 +101,4 @@ def test_committed_bench_line_keeps_the_contract():
     assert fast["value"] > line["value"] and fast["pixels_differing_from_headline_image"] < 1e-3
     fr = fast["roofline"]
     assert fr["bound"] == "vmem" and fr["counters_library_matches"] is True
-    assert fr["counters_from"] == "profiles/r06_sah_C3_summary.json" and (ROOT / fr["counters_from"]).exists()
+    assert fr["counters_from"] == "profiles/r06f_sah_C3_summary.json" and (ROOT / fr["counters_from"]).exists()
