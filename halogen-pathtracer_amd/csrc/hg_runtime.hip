@@ -1007,10 +1007,13 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     if (!rc) rc = ensure_uncached(c, S.done, size_t(ring) * 128u);
     if (!rc) rc = ensure_uncached(c, S.ctl, HG_SV_CTL_BYTES);  // (polled by scalar loads: hg_mega.hip sv_sload)
     if (!rc && spill_bytes) rc = ensure(c, S.spill, spill_bytes);
-    if (!rc && c->tile_order_on) rc = ensure(c, S.tile_cost, 2 * tb);
-    if (!rc && c->tile_order_on) rc = ensure(c, S.tile_order, tb);
+    // the cost order only with HG_SV_COST_ORDER: the server's frames overlap, so no frame's end waits on its longest
+    // tiles, and raster order keeps a claim's consecutive tiles together (HG_SV_COST_ORDER in hg_layout.h)
+    const bool ordered = c->tile_order_on && HG_SV_COST_ORDER;
+    if (!rc && ordered) rc = ensure(c, S.tile_cost, 2 * tb);
+    if (!rc && ordered) rc = ensure(c, S.tile_order, tb);
     const size_t osb = hg_order_scratch_bytes(tiles);
-    if (!rc && c->tile_order_on && S.order_scratch.bytes < osb) {
+    if (!rc && ordered && S.order_scratch.bytes < osb) {
         rc = ensure(c, S.order_scratch, osb);
         if (!rc && hipMemsetAsync(S.order_scratch.p, 0, S.order_scratch.bytes, S.stream) != hipSuccess)
             rc = fail(c, HG_E_HIP, "hipMemsetAsync(server order scratch) failed");
@@ -1029,7 +1032,7 @@ int server_start(hg_ctx* c, const HgKernelParams& kp_in, int32_t fc) {
     HgKernelParams kp = kp_in;
     kp.tile_order = nullptr;
     kp.tile_cost = nullptr;
-    if (c->tile_order_on) {
+    if (ordered) {
         kp.tile_cost = static_cast<unsigned long long*>(S.tile_cost.p);
         if (S.tile_cost_valid) {  // the cost order of the last lifetime's frames
             HG_HIP(c, hg_launch_order_tiles(kp.tile_cost, static_cast<uint32_t*>(S.tile_order.p), tiles, S.order_scratch.p,
