@@ -486,7 +486,9 @@ def strong_scaling_measurement(ctx, params, W, H, fps: int, steps: int, world: i
            "ms_per_step": dt_max * 1e3 / steps,
            "per_rank": [{"rank": r, "tiles": int(v[2]), "trace_ms_per_step": v[1] * 1e3 / steps,
                          "total_ms_per_step": v[0] * 1e3 / steps, "trace_busy_ms": v[3]} for r, v in enumerate(per_rank)],
-           "trace_balance": min(v[1] for v in per_rank) / max(v[1] for v in per_rank)}
+           "trace_balance": min(v[1] for v in per_rank) / max(v[1] for v in per_rank),
+           # a share holds consecutive calls until its launch fills the GPU (HG_OPT_COALESCE's share window)
+           "launches": int(c.get("launches", 0))}
     if emu:
         res["emulated"] = f"rank 0's share of {n} on one GPU: value is that share's rate; x{n} if every share ran alike"
         res["value_if_balanced"] = res["value"] * n
