@@ -187,7 +187,7 @@
 // The render server's units in the cost order of its last lifetime's frames (1) or in raster order with no cost records
 // (0).  The cost order puts a launch's longest tiles first so that its end waits less on them; the server's frames
 // overlap, so there is no such end, and raster order keeps a claim's consecutive tiles together.  C3, server forced,
-// one box, two rounds (tools/gpu_server_order.sh): strict 3,155 / 3,159 -> 3,168 / 3,164, display at once (R11G11B10F)
+// one box, two rounds (tools/sweeps/sweep_r06_server_order.txt): strict 3,155 / 3,159 -> 3,168 / 3,164, display at once (R11G11B10F)
 // 2,662 / 2,669 -> 2,752 / 2,726 Mpaths/s.
 #define HG_SV_COST_ORDER 0
 #endif
