@@ -191,6 +191,15 @@
 // 2,662 / 2,669 -> 2,752 / 2,726 Mpaths/s.
 #define HG_SV_COST_ORDER 0
 #endif
+#ifndef HG_SV_TILE_RUN
+// The render server's XCD heads take runs of this many consecutive tiles (hg_mega.hip sv_pull): head h (the XCD whose
+// waves pull it first) runs h, h + 8, ..., so a CU's waves pull neighbouring tiles and the heads still interleave
+// finely over the frame (one contiguous band per head lost 1-3 %: per-XCD balance).  C3, server forced, one box, two
+// rounds (tools/sweeps/sweep_r06_server_runs.txt), runs of 1 / 4 / 8 / 16: strict 3,169-3,176 / 3,183-3,194 /
+// 3,187-3,193 / 3,181-3,183, display at once 2,643-2,714 / 2,706-2,716 / 2,724-2,735 / 2,701, one behind
+// 2,811-2,847 / 2,837-2,868 / 2,879-2,881 / 2,789-2,862 Mpaths/s.
+#define HG_SV_TILE_RUN 8u
+#endif
 #ifndef HG_SV_CLAIM
 #define HG_SV_CLAIM 4u  // units per claim of a server wave far behind the posted units (the rest held for its next pulls)
 #endif

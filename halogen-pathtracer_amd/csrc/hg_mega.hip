@@ -1096,7 +1096,17 @@ __device__ void sv_pull(const HgKernelParams& kp, uint32_t slot, uint32_t base) 
     if (HG_SV_DIAG_TIMES && k < 256u)  // (analysis builds) the frame's first claim: max of the complement
         __hip_atomic_fetch_max(sv_word64(kp, HG_SV_DIAG_WORD + 4u * k), ~(unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int tile = ordered_tile(kp, u - k * lds_get(hg_sv.nlt));
+    uint32_t i = u - k * lds_get(hg_sv.nlt);  // the unit's place in its frame
+    if (HG_SV_TILE_RUN > 1u && !kp.tile_order) {
+        // runs: head h (u % 8, the XCD whose waves pull it first) takes runs h, h + 8, ... of HG_SV_TILE_RUN consecutive
+        // tiles, so a wave's and a CU's consecutive units are neighbours (the tail past the last whole round in place)
+        constexpr uint32_t B = HG_SV_TILE_RUN;
+        if (i < (lds_get(hg_sv.nlt) / (8u * B)) * (8u * B)) {
+            const uint32_t h = i & 7u, n = i >> 3;
+            i = (n / B) * (8u * B) + h * B + n % B;
+        }
+    }
+    const int tile = ordered_tile(kp, i);
     const uint32_t g = uint32_t(kp.rank) + uint32_t(tile) * uint32_t(kp.n_ranks);
     const uint32_t ty = g / uint32_t(kp.tiles_x);
     const uint32_t tx0 = (g - ty * uint32_t(kp.tiles_x)) * HG_TILE, ty0 = ty * HG_TILE;
